@@ -1,0 +1,251 @@
+"""Benchmark: perturbation-samples/s of the XP-GNN hot path on MI355X (BASELINE.json metric).
+
+Workload (configs[1] of BASELINE.json, "c2"): synthetic homogeneous graph, 100k nodes / 1M
+edges, 64-dim fp32 features, 2-layer GCN 64->64->64 + Linear(64->1) + sigmoid (random init),
+interpret_samples=256, epochs=50 -> 12,800 mask rows per repeat, query node 7 (node_prediction:
+its 3-hop computational subgraph, as the reference extracts it).
+
+One step = one full repeat of the hot path per rank, inputs resident in HBM:
+  device mask sampling (Philox Shapley rows) -> masked receptive-field forward (all rows) ->
+  KernelSHAP weights -> surrogate Adam loop (ceil(R / (R // epochs)) steps) ->
+  (N > 1) all-gather of the per-repeat weights for the mean/std over repeats.
+Repeats are independent, so ranks shard repeats (weak scaling, one repeat per rank per step).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "perturbation-samples/sec (masked GNN fwd) per query node; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--nodes", type=int, default=100_000)
+    p.add_argument("--edges", type=int, default=1_000_000)
+    p.add_argument("--feat", type=int, default=64)
+    p.add_argument("--interpret-samples", type=int, default=256)
+    p.add_argument("--epochs", type=int, default=50)
+    p.add_argument("--query", type=int, default=7)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-rows", type=int, default=2560)
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def build_workload(args, dev):
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.data import Data
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+
+    g = torch.Generator().manual_seed(0)
+    feat = torch.randn((args.nodes, args.feat), generator=g)
+    ei = torch.randint(0, args.nodes, (2, args.edges), generator=g)
+    torch.manual_seed(0)
+    arch = ConvStack("gcn", [args.feat, 64, 64], [64, 1]).eval().to(dev)
+    data = Data(feat.to(dev), ei.to(dev))
+    names = [str(i) for i in range(args.nodes)]
+    sub_feat, sub_ei, _, sub_ind, _, _ = data.comp_graph(args.query, 2, "node", names)
+    q = int(sub_ind.reshape(-1)[0])
+    plan = pipeline.build_plan(arch, sub_feat, sub_ei, [q])
+    return arch, sub_feat, sub_ei, q, plan
+
+
+def forward_bytes(plan, rows):
+    """Algorithmic HBM bytes of the masked forward per launch chain: per row,
+    per layer: CSR pointers + columns of the targets, the row's mask words, the gathered
+    source rows of kept edges + self rows (F_out wide, layer-1 tables), the written outputs."""
+    arr = plan.arrays
+    W = (plan.cols + 31) // 32
+    b = 4 * (plan.n0 + 1) + 4 * arr["deg_src"].size + 4 * W  # degree pass
+    for li, conv in enumerate(plan.program.convs):
+        lay = arr["layers"][li]
+        n_t = arr["frontiers"][li + 1].size
+        e = lay["agg_src"].size
+        width = conv.f_out if li == 0 else conv.f_in
+        b += 4 * (n_t + 1) + 8 * e + 4 * width * (0.25 * e + n_t) + 4 * conv.f_out * n_t
+    return b * rows
+
+
+def wlm_bytes(rows, cols, batch):
+    W = (cols + 31) // 32
+    return rows * W * 4 + rows * (4 + 8) + cols * 4 * 6 + 8 * math.ceil(rows / batch)
+
+
+def cpu_baseline(args, arch, sub_feat, sub_ei, q):
+    """The numpy oracle (CPU restatement of the reference path, 1 thread) on a bounded sample
+    of the same workload: cpu_rows mask rows through forward + KernelSHAP + surrogate."""
+    import oracle
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    S = sub_feat.shape[0]
+    rows = args.cpu_rows
+    rng = np.random.default_rng(0)
+    m = rng.random((rows, S)) < 0.5
+    spec = {"convs": [{"kind": "gcn", "rels": [None], "act": "relu",
+                       "params": {None: {"W": arch.conv[2 * i].lin.weight.detach().cpu().numpy(),
+                                         "b": arch.conv[2 * i].bias.detach().cpu().numpy()}}}
+                      for i in range(2)],
+            "fc": [{"W": arch.fc[0].weight.detach().cpu().numpy(),
+                    "b": arch.fc[0].bias.detach().cpu().numpy(), "act": "sigmoid"}]}
+    x = sub_feat.cpu().numpy()
+    e = {None: sub_ei.cpu().numpy()}
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    try:
+        t0 = time.perf_counter()
+        y = oracle.masked_query_outputs(spec, x, e, m, q, dtype=np.float32)
+        k = oracle.shap_kernel(m)
+        oracle.train_wlm(m, args.interpret_samples, y, k, np.zeros(S, np.float32),
+                         {"lr": 0.01, "l1_lambda": 1e-4}, dtype=np.float32)
+        dt = time.perf_counter() - t0
+    finally:
+        if ctx is not None:
+            ctx.unregister() if hasattr(ctx, "unregister") else None
+    return {"value": rows / dt, "unit": "samples/s", "cores": 1, "kind": "port",
+            "sample": f"{rows} mask rows of the same workload (S={S}) through the numpy oracle "
+                      f"(union-graph forward + KernelSHAP + surrogate fit), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    from bikg_graph_explainability_public_amd import _lib, engine
+
+    _lib.load()
+    arch, sub_feat, sub_ei, q, plan = build_workload(args, dev)
+    S = plan.cols
+    R = args.interpret_samples * args.epochs
+    batch = R // args.epochs
+    w0 = torch.zeros(S)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    stream = torch.cuda.current_stream()
+    ev = {k: [] for k in ("sample", "forward", "shap", "wlm")}
+
+    def step(i, record):
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
+        if record:
+            marks[0].record(stream)
+        bits = engine.sample_shapley(1000 + i * world + rank, R, S, dev)
+        if record:
+            marks[1].record(stream)
+        y = plan.forward(bits)[:, 0]
+        if record:
+            marks[2].record(stream)
+        k = engine.shap_kernel(bits, S)
+        if record:
+            marks[3].record(stream)
+        w, _, _, _, _ = engine.wlm_fit(bits, S, batch, y, k, w0, params)
+        if record:
+            marks[4].record(stream)
+            for j, name in enumerate(("sample", "forward", "shap", "wlm")):
+                ev[name].append((marks[j], marks[j + 1]))
+        if world > 1:
+            import torch.distributed as dist
+            out = [torch.empty_like(w) for _ in range(world)]
+            dist.all_gather(out, w)
+            st = torch.stack(out)
+            return st.mean(0), st.std(0, unbiased=False)
+        return w, None
+
+    for i in range(args.warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    phase_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+
+    if rank == 0:
+        total_rows = R * world * args.steps
+        dominant = max(phase_ms, key=phase_ms.get)
+        if dominant == "wlm":
+            bytes_launch = wlm_bytes(R, S, batch)
+            kname = "k_wlm (surrogate Adam loop, 1 persistent workgroup)"
+        elif dominant == "forward":
+            bytes_launch = forward_bytes(plan, R)
+            kname = "masked forward chain (k_degree + k_agg + k_dense + k_take_col)"
+        elif dominant == "shap":
+            bytes_launch = R * ((S + 31) // 32) * 4 + R * 12
+            kname = "k_popcount + k_shap"
+        else:
+            bytes_launch = R * ((S + 31) // 32) * 4
+            kname = "k_shapley"
+        achieved = bytes_launch / (phase_ms[dominant] * 1e-3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": total_rows / elapsed,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {"workload": "c2: synthetic homogeneous 100k nodes / 1M edges, 64-dim "
+                                   "feats, 2-layer GCN, interpret_samples=256, node_prediction "
+                                   "(3-hop computational subgraph of node 7)",
+                       "nodes": args.nodes, "edges": args.edges, "feat": args.feat,
+                       "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
+                       "interpret_samples": args.interpret_samples, "epochs": args.epochs,
+                       "rows_per_repeat": R, "repeats_per_step": world,
+                       "parallelism": f"repeats sharded over {world} rank(s)",
+                       "mask_sampler": "device (Philox Shapley)"},
+            "phases_ms": phase_ms,
+            "roofline": {"kernel": kname, "bound": "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "bytes_per_launch": bytes_launch},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, arch, sub_feat, sub_ei, q)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,850 @@
+// xpgnn.hip — MI355X (gfx950, CDNA4) kernels + C-ABI of the XP-GNN perturbation-scoring engine.
+//
+// Hot path: mask rows (bit-packed) -> masked k-hop message passing restricted to
+// the query's receptive field (frontiers F_L ⊆ ... ⊆ F_0) -> dense head -> per-row query logit;
+// KernelSHAP weights from row popcounts; the weighted linear surrogate's whole Adam epoch loop in
+// one persistent workgroup.  See include/xpgnn.h for the interface and DESIGN.md for layouts.
+//
+// Conventions: wave64; 256-thread blocks unless noted; fp32 activations/weights, fp64 kernel
+// weights and loss (as the reference); dense contractions on the f32-input MFMA
+// (v_mfma_f32_32x32x2_f32: exact fp32 fma chains, no reduced-precision path).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "../../include/xpgnn.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define XPG_HIP(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return fail(XPG_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define XPG_LAUNCHED() XPG_HIP(hipGetLastError())
+
+#define XPG_REQ(cond, msg)                          \
+  do {                                              \
+    if (!(cond)) return fail(XPG_EINVAL, (msg));    \
+  } while (0)
+
+inline hipStream_t S(xpg_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int words_of(int64_t cols) { return static_cast<int>((cols + 31) / 32); }
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ bool bit_of(const uint32_t* row, int c) {
+  return (row[c >> 5] >> (c & 31)) & 1u;
+}
+
+__device__ __forceinline__ float act_apply(float x, int act) {
+  switch (act) {
+    case XPG_ACT_RELU: return x > 0.f ? x : 0.f;
+    case XPG_ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+    case XPG_ACT_TANH: return tanhf(x);
+    case XPG_ACT_LEAKY_RELU: return x > 0.f ? x : 0.01f * x;
+    case XPG_ACT_ELU: return x > 0.f ? x : expm1f(x);
+    default: return x;
+  }
+}
+
+// ------------------------------------------------------------------------------------ masks
+__global__ void k_pack(const uint8_t* __restrict__ m, int64_t rows, int64_t cols, int words,
+                       uint32_t* __restrict__ bits) {
+  int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (idx >= rows * words) return;
+  int64_t r = idx / words;
+  int w = static_cast<int>(idx - r * words);
+  const uint8_t* p = m + r * cols + (int64_t)w * 32;
+  int n = static_cast<int>(cols - (int64_t)w * 32);
+  n = n > 32 ? 32 : n;
+  uint32_t v = 0;
+  for (int i = 0; i < n; ++i) v |= (p[i] ? 1u : 0u) << i;
+  bits[idx] = v;
+}
+
+__global__ void k_unpack(const uint32_t* __restrict__ bits, int64_t rows, int64_t cols, int words,
+                         uint8_t* __restrict__ m) {
+  int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (idx >= rows * cols) return;
+  int64_t r = idx / cols;
+  int64_t c = idx - r * cols;
+  m[idx] = (bits[r * words + (c >> 5)] >> (c & 31)) & 1u;
+}
+
+// Philox4x32-10 (Salmon et al., SC'11): counter-based, so any row range can be regenerated
+// independently (multi-GPU shards draw disjoint global rows).
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__global__ void k_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
+                          int words, uint32_t* __restrict__ bits) {
+  const int quads = (words + 3) / 4;
+  int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (idx >= rows * quads) return;
+  int64_t r = idx / quads;
+  int q = static_cast<int>(idx - r * quads);
+  uint64_t gr = (uint64_t)(row_offset + r);
+  uint4 o = philox4x32_10(make_uint4((uint32_t)q, (uint32_t)gr, (uint32_t)(gr >> 32), 0x58504721u),
+                          (uint32_t)seed, (uint32_t)(seed >> 32));
+  uint32_t v[4] = {o.x, o.y, o.z, o.w};
+  const int tail = static_cast<int>(cols & 31);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int w = q * 4 + j;
+    if (w < words) {
+      uint32_t x = v[j];
+      if (w == words - 1 && tail) x &= (1u << tail) - 1u;
+      bits[r * words + w] = x;
+    }
+  }
+}
+
+__global__ void k_edge_keep(const uint32_t* __restrict__ bits, int64_t rows, int words,
+                            const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                            int64_t n_edges, uint8_t* __restrict__ keep) {
+  int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (idx >= rows * n_edges) return;
+  int64_t b = idx / n_edges;
+  int64_t e = idx - b * n_edges;
+  const uint32_t* row = bits + b * words;
+  keep[idx] = static_cast<uint8_t>(bit_of(row, src[e]) && bit_of(row, dst[e]));
+}
+
+// ------------------------------------------------------------------------------------ KernelSHAP
+// one wave per row: lanes stride the row's words, popcount, wave-reduce.
+__global__ void k_popcount(const uint32_t* __restrict__ bits, int64_t rows, int words,
+                           int32_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  int64_t r = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const uint32_t* row = bits + r * words;
+  int c = 0;
+  for (int w = lane; w < words; w += 64) c += __popc(row[w]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if (lane == 0) counts[r] = c;
+}
+
+// scipy.special.binom for integer-valued n >= 0, k (kernels.py:64,109 call sites): the product
+// formula below 20 (bit-identical to scipy), the Gamma form otherwise (~1e-13 relative).
+__device__ double binom_d(double n, double k) {
+  if (k < 0.0 || k > n) return 0.0;
+  double kx = k;
+  if (kx > n / 2 && n > 0) kx = n - kx;
+  if (kx >= 0 && kx < 20) {
+    double num = 1.0, den = 1.0;
+    const int kk = static_cast<int>(kx);
+    for (int i = 1; i < 1 + kk; ++i) {
+      num *= i + n - kx;
+      den *= i;
+      if (fabs(num) > 1e50) {
+        num /= den;
+        den = 1.0;
+      }
+    }
+    return num / den;
+  }
+  return exp(lgamma(n + 1.0) - lgamma(k + 1.0) - lgamma(n - k + 1.0));
+}
+
+__device__ __forceinline__ double clean_inf(double v) { return (isinf(v) || isnan(v)) ? 0.0 : v; }
+
+__device__ double block_sum_d(double v, double* red) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+// Kernel.compute (kernels.py:115-174).  Exact branch is row-parallel; the approximate branch
+// runs the reference's ref back-off loop (sum == 0 -> ref = int(0.9 ref)) in this one block.
+__global__ __launch_bounds__(1024) void k_shap(const int32_t* __restrict__ cnt, int64_t rows,
+                                               int64_t cols, double* __restrict__ out) {
+  __shared__ double red[16];
+  const int64_t Mi = cols - 1;
+  const double M = static_cast<double>(Mi);
+  if (Mi <= 1000) {
+    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) {
+      const int64_t k = cnt[r];
+      const double choose = binom_d(M + 1.0, static_cast<double>(k));
+      out[r] = clean_inf(M / (choose * static_cast<double>(Mi + 1 - k) * static_cast<double>(k)));
+    }
+    return;
+  }
+  int ref = 1000;
+  for (;;) {
+    double part = 0.0;
+    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) {
+      const int64_t k = cnt[r];
+      int64_t idx = static_cast<int64_t>(static_cast<float>(k * 1000) / static_cast<float>(Mi));
+      idx = idx < 0 ? 0 : (idx > ref - 1 ? ref - 1 : idx);
+      const double choose = (binom_d(static_cast<double>(ref), static_cast<double>(idx)) + 1e-10) * M / 1000.0;
+      const double v = M / (choose * static_cast<double>(k) * static_cast<double>(Mi - k));
+      out[r] = v;
+      part += v;
+    }
+    const double sum = block_sum_d(part, red);
+    if (sum > 0.0) break;
+    ref = static_cast<int>(0.9 * static_cast<double>(ref));
+    if (!(sum == 0.0 && ref > 0)) break;
+  }
+  __syncthreads();
+  for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) out[r] = clean_inf(out[r]);
+}
+
+// ------------------------------------------------------------------------------------ dense
+// C = act(A W^T + b) on v_mfma_f32_32x32x2_f32.  One wave owns 32 rows x (NT*32) columns; the
+// k loop advances 8 at a time: each lane loads one float4 of its A row and one float4 of each
+// W row, feeding 4 MFMAs whose 2 k-slots map to k = kc + 4*h + s (h = lane >> 5), identically
+// for A and B, so the contraction is exact.  C/D map: col = lane & 31,
+// row = (reg & 3) + 8 * (reg >> 2) + 4 * h.
+template <int NT>
+__global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int64_t M, int64_t lda,
+                                               const float* __restrict__ W, int64_t ldw, int k_pad,
+                                               const float* __restrict__ bias, int n_real, int act,
+                                               float* __restrict__ C, int64_t ldc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m0 = (blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 32;
+  if (m0 >= M) return;
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t arow = m0 + i;
+  const bool a_ok = arow < M;
+  const float* ap = A + (a_ok ? arow : 0) * lda + 4 * h;
+  f32x16 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
+  for (int kc = 0; kc < k_pad; kc += 8) {
+    float4 a = a_ok ? *reinterpret_cast<const float4*>(ap + kc) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const float4 w = *reinterpret_cast<const float4*>(W + (int64_t)(nt * 32 + i) * ldw + kc + 4 * h);
+      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w.x, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w.y, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, w.z, acc[nt], 0, 0, 0);
+      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, w.w, acc[nt], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = nt * 32 + i;
+    const float bv = col < n_real ? bias[col] : 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int64_t m = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (m < M) C[m * ldc + col] = col < n_real ? act_apply(acc[nt][reg] + bv, act) : 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------ forward
+// kin[(b * n_rel + r) * n0 + p] = kept in-degree of F_0 node p under relation r for mask row b
+// (self-loops excluded), or -1 when the node itself is masked out (then it keeps only the
+// GCN self-loop / an empty SAGE neighbourhood).
+__global__ void k_degree(const uint32_t* __restrict__ bits, int64_t rows, int words, int n0,
+                         int n_rel, const int32_t* __restrict__ f0_node,
+                         const int32_t* __restrict__ deg_ptr, const int32_t* __restrict__ deg_src,
+                         float* __restrict__ kin) {
+  const int64_t per_row = (int64_t)n_rel * n0;
+  int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (idx >= rows * per_row) return;
+  const int64_t b = idx / per_row;
+  const int rem = static_cast<int>(idx - b * per_row);
+  const int r = rem / n0, p = rem - r * n0;
+  const uint32_t* row = bits + b * words;
+  float out = -1.f;
+  if (bit_of(row, f0_node[p])) {
+    const int* pp = deg_ptr + (int64_t)r * (n0 + 1);
+    int c = 0;
+    for (int e = pp[p]; e < pp[p + 1]; ++e) c += bit_of(row, deg_src[e]);
+    out = static_cast<float>(c);
+  }
+  kin[idx] = out;
+}
+
+struct AggArgs {
+  int64_t rows;
+  int n0, n_rel, n_tgt, n_prev;
+  const float* kin;
+  const int32_t* tgt_prev;
+  const int32_t* tgt_f0;
+  const int32_t* agg_ptr;
+  const int32_t* agg_src;
+  const int32_t* agg_f0;
+  const int32_t* self_mult;
+  int n_terms;
+  int kind[XPG_MAX_TERMS];
+  int rel[XPG_MAX_TERMS];
+  const float* table[XPG_MAX_TERMS];
+  const float* hprev;   // layer >= 2 source rows [rows][n_prev][width]
+  int width;            // source row width (floats, % 32 == 0)
+  float* out;
+  int64_t out_ld;
+  const float* bias;    // layer 1 epilogue
+  int act;
+  int f_real;
+};
+
+__device__ __forceinline__ float inv_sqrt_deg(float kin) {
+  return 1.f / sqrtf(1.f + (kin > 0.f ? kin : 0.f));
+}
+
+__device__ __forceinline__ void fma4(float4& a, float c, const float4 v) {
+  a.x = fmaf(c, v.x, a.x);
+  a.y = fmaf(c, v.y, a.y);
+  a.z = fmaf(c, v.z, a.z);
+  a.w = fmaf(c, v.w, a.w);
+}
+
+// Masked aggregation for one conv layer.  Item = (mask row b, target t); LPS lanes per item,
+// each lane owns NV float4 feature chunks.  L1: sources are the shared pre-transformed F_0
+// tables (X W^T computed once per query: features are never masked, data.py:582) and the
+// epilogue applies bias + activation; otherwise sources are the previous layer's per-row
+// outputs and each term's aggregate is written to its slice of the GEMM input.
+template <bool L1, int LPS, int NV>
+__global__ __launch_bounds__(256) void k_agg(AggArgs a) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t item = gid / LPS;
+  const int sub = static_cast<int>(gid - item * LPS);
+  if (item >= a.rows * a.n_tgt) return;
+  const int64_t b = item / a.n_tgt;
+  const int t = static_cast<int>(item - b * a.n_tgt);
+  const float* kb = a.kin + b * (int64_t)a.n_rel * a.n0;
+  const int t0 = a.tgt_f0[t];
+  const int tp = a.tgt_prev[t];
+  float4 tot[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) tot[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  for (int k = 0; k < a.n_terms; ++k) {
+    const int kind = a.kind[k];
+    const int r = a.rel[k];
+    const float* base = L1 ? a.table[k] : a.hprev + b * (int64_t)a.n_prev * a.width;
+    const int self_pos = L1 ? t0 : tp;
+    const float4* selfrow = reinterpret_cast<const float4*>(base + (int64_t)self_pos * a.width);
+    float4 s[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) s[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (kind == XPG_TERM_ROOT) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) s[j] = selfrow[sub + j * LPS];
+    } else {
+      const float kt = kb[(int64_t)r * a.n0 + t0];
+      const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+      if (kind == XPG_TERM_GCN) {
+        const float dt = inv_sqrt_deg(kt);
+        const float cself = dt * dt;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) fma4(s[j], cself, selfrow[sub + j * LPS]);
+        if (kt >= 0.f) {
+          for (int e = pp[t]; e < pp[t + 1]; ++e) {
+            const int u0 = a.agg_f0[e];
+            const float ku = kb[(int64_t)r * a.n0 + u0];
+            if (ku >= 0.f) {
+              const float c = inv_sqrt_deg(ku) * dt;
+              const int up = L1 ? u0 : a.agg_src[e];
+              const float4* src = reinterpret_cast<const float4*>(base + (int64_t)up * a.width);
+#pragma unroll
+              for (int j = 0; j < NV; ++j) fma4(s[j], c, src[sub + j * LPS]);
+            }
+          }
+        }
+      } else {  // MEAN
+        if (kt >= 0.f) {
+          const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+          const float cnt = kt + static_cast<float>(sm);
+#pragma unroll
+          for (int j = 0; j < NV; ++j) fma4(s[j], static_cast<float>(sm), selfrow[sub + j * LPS]);
+          for (int e = pp[t]; e < pp[t + 1]; ++e) {
+            const int u0 = a.agg_f0[e];
+            if (kb[(int64_t)r * a.n0 + u0] >= 0.f) {
+              const int up = L1 ? u0 : a.agg_src[e];
+              const float4* src = reinterpret_cast<const float4*>(base + (int64_t)up * a.width);
+#pragma unroll
+              for (int j = 0; j < NV; ++j) {
+                const float4 v = src[sub + j * LPS];
+                s[j].x += v.x; s[j].y += v.y; s[j].z += v.z; s[j].w += v.w;
+              }
+            }
+          }
+          const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
+#pragma unroll
+          for (int j = 0; j < NV; ++j) { s[j].x *= inv; s[j].y *= inv; s[j].z *= inv; s[j].w *= inv; }
+        }
+      }
+    }
+    if (L1) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        tot[j].x += s[j].x; tot[j].y += s[j].y; tot[j].z += s[j].z; tot[j].w += s[j].w;
+      }
+    } else {
+      float4* o = reinterpret_cast<float4*>(a.out + item * a.out_ld + (int64_t)k * a.width);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) o[sub + j * LPS] = s[j];
+    }
+  }
+  if (L1) {
+    float4* o = reinterpret_cast<float4*>(a.out + item * a.out_ld);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int f = (sub + j * LPS) * 4;
+      float v[4] = {tot[j].x, tot[j].y, tot[j].z, tot[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = (f + q < a.f_real) ? act_apply(v[q] + a.bias[f + q], a.act) : 0.f;
+      o[sub + j * LPS] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+__global__ void k_take_col(const float* __restrict__ C, int64_t M, int64_t ldc, int col,
+                           float* __restrict__ y) {
+  int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (m < M) y[m] = C[m * ldc + col];
+}
+
+// ------------------------------------------------------------------------------------ surrogate
+// train_model (wlm.py:132-278) in one persistent 1024-thread workgroup: every Adam step's batch
+// of mask words is staged transposed in LDS ([word][row], odd row pitch), predictions are
+// bit-scans over w (LDS, 33-float pitch per 32 columns), the loss/gradient use the reference's
+// [B] - [B,1] broadcast in closed form (quirk Q1), parameters stay in registers (CPT per thread).
+template <int CPT>
+__global__ __launch_bounds__(1024) void k_wlm(const uint32_t* __restrict__ bits, int64_t rows,
+                                              int cols, int words, int batch, int pitch,
+                                              const float* __restrict__ y,
+                                              const double* __restrict__ kern, xpg_wlm_params P,
+                                              int64_t step0, float* __restrict__ wg,
+                                              float* __restrict__ mg, float* __restrict__ vg,
+                                              double* __restrict__ losses,
+                                              int32_t* __restrict__ best_epoch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* red = reinterpret_cast<double*>(smem);                 // [32]
+  float* w_s = reinterpret_cast<float*>(smem + 256);              // [words * 33]
+  float* p_s = w_s + ((words * 33 + 3) & ~3);                     // [pitch]
+  float* g_s = p_s + pitch;                                       // [pitch]
+  uint32_t* wt = reinterpret_cast<uint32_t*>(g_s + pitch);        // [words][pitch]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
+
+  float w[CPT], m[CPT], v[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int i = tid + c * 1024;
+    w[c] = i < cols ? wg[i] : 0.f;
+    m[c] = i < cols ? mg[i] : 0.f;
+    v[c] = i < cols ? vg[i] : 0.f;
+  }
+  const int64_t nsteps = (rows + batch - 1) / batch;
+  double best = INFINITY;
+  int best_e = 0;
+  const float inv_cols = 1.f / static_cast<float>(cols);
+  for (int64_t t = 0; t < nsteps; ++t) {
+    const int64_t r0 = t * batch;
+    const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+    // stage batch words transposed (zero the row padding) and the current w
+    for (int idx = tid; idx < words * pitch; idx += blockDim.x) {
+      const int wd = idx / pitch, j = idx - wd * pitch;
+      wt[idx] = j < B ? bits[(r0 + j) * words + wd] : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int i = tid + c * 1024;
+      if (i < cols) w_s[(i >> 5) * 33 + (i & 31)] = w[c];
+    }
+    __syncthreads();
+    // predictions p_j = sum_i M[j,i] w_i
+    for (int j = wv; j < B; j += nwv) {
+      float s = 0.f;
+      for (int wd = lane; wd < words; wd += 64) {
+        uint32_t word = wt[wd * pitch + j];
+        const float* wb = w_s + wd * 33;
+        while (word) {
+          const int c = __ffs(word) - 1;
+          s += wb[c];
+          word &= word - 1u;
+        }
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+      if (lane == 0) p_s[j] = s;
+    }
+    // per-step constants (independent of w): sum y, sum k
+    double sy = 0.0, sk = 0.0, sa = 0.0;
+    for (int j = tid; j < B; j += blockDim.x) {
+      sy += static_cast<double>(y[r0 + j]);
+      sk += kern[r0 + j];
+    }
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) sa += fabs(static_cast<double>(w[c]));
+    const double Sy = block_sum_d(sy, red);
+    const double Sk = block_sum_d(sk, red);
+    const double Sa = block_sum_d(sa, red);
+    const double ybar = Sy / B;
+    double vy = 0.0, tk = 0.0;
+    for (int j = tid; j < B; j += blockDim.x) {
+      const double dy = static_cast<double>(y[r0 + j]) - ybar;
+      const double dp = static_cast<double>(p_s[j]) - ybar;
+      const double kj = kern[r0 + j];
+      vy += dy * dy;
+      tk += kj * dp * dp;
+      g_s[j] = static_cast<float>(2.0 * kj * dp / (static_cast<double>(B) * Sk));
+    }
+    for (int j = B + tid; j < pitch; j += blockDim.x) g_s[j] = 0.f;
+    const double Vy = block_sum_d(vy, red);
+    const double Tk = block_sum_d(tk, red);
+    // loss = mean_ij k_j (p_j - y_i)^2 / sum k + l1 * mean|w|   (wlm.py:240-243, 517-518)
+    const float reg = P.l1_lambda * static_cast<float>(Sa / cols);
+    const double loss = Tk / (static_cast<double>(B) * Sk) + Vy / (static_cast<double>(B) * B) +
+                        static_cast<double>(reg);
+    // gradient + Adam (torch single-tensor Adam with L2 weight decay)
+    const int64_t step = step0 + t + 1;
+    const double bc1 = 1.0 - pow(static_cast<double>(P.beta1), static_cast<double>(step));
+    const double bc2 = 1.0 - pow(static_cast<double>(P.beta2), static_cast<double>(step));
+    const float step_size = static_cast<float>(static_cast<double>(P.lr) / bc1);
+    const float bc2_sqrt = static_cast<float>(sqrt(bc2));
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int i = tid + c * 1024;
+      if (i < cols) {
+        const uint32_t* col = wt + (i >> 5) * pitch;
+        const int bit = i & 31;
+        float s = 0.f;
+        for (int j = 0; j < B; j += 4) {
+          const uint4 q = *reinterpret_cast<const uint4*>(col + j);
+          const float4 gq = *reinterpret_cast<const float4*>(g_s + j);
+          s += ((q.x >> bit) & 1u) ? gq.x : 0.f;
+          s += ((q.y >> bit) & 1u) ? gq.y : 0.f;
+          s += ((q.z >> bit) & 1u) ? gq.z : 0.f;
+          s += ((q.w >> bit) & 1u) ? gq.w : 0.f;
+        }
+        const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
+        float g = s + P.l1_lambda * inv_cols * sg;
+        g = fmaf(P.weight_decay, w[c], g);
+        m[c] = fmaf(1.f - P.beta1, g - m[c], m[c]);
+        v[c] = fmaf(1.f - P.beta2, g * g, v[c] * P.beta2);
+        const float denom = sqrtf(v[c]) / bc2_sqrt + P.eps;
+        w[c] = w[c] - step_size * (m[c] / denom);
+      }
+    }
+    if (tid == 0) {
+      losses[t] = loss;
+      if (loss < best) {
+        best = loss;
+        best_e = static_cast<int>(t);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int i = tid + c * 1024;
+    if (i < cols) {
+      wg[i] = w[c];
+      mg[i] = m[c];
+      vg[i] = v[c];
+    }
+  }
+  if (tid == 0) best_epoch[0] = best_e;
+}
+
+// ------------------------------------------------------------------------------------ helpers
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct WsLayout {
+  size_t kin = 0, agg = 0, head0 = 0, head1 = 0, total = 0;
+  size_t h[64];
+};
+
+int layout_ws(const xpg_forward_plan* p, int64_t rows, WsLayout* L) {
+  XPG_REQ(p && p->n_layers >= 1 && p->n_layers <= 64, "plan: 1..64 conv layers required");
+  size_t off = 0;
+  L->kin = off;
+  off += align_up(sizeof(float) * (size_t)rows * p->n_rel * p->n0);
+  size_t agg_max = 0;
+  for (int l = 0; l < p->n_layers; ++l) {
+    const xpg_layer_desc& ly = p->layers[l];
+    L->h[l] = off;
+    off += align_up(sizeof(float) * (size_t)rows * ly.n_tgt * ly.f_out_pad);
+    if (l > 0) {
+      size_t a = sizeof(float) * (size_t)rows * ly.n_tgt * ly.n_terms * ly.f_in_pad;
+      agg_max = a > agg_max ? a : agg_max;
+    }
+  }
+  L->agg = off;
+  off += align_up(agg_max);
+  size_t hmax = 0;
+  const int64_t n_last = p->layers[p->n_layers - 1].n_tgt;
+  for (int i = 0; i < p->n_head; ++i) {
+    size_t hb = sizeof(float) * (size_t)rows * n_last * p->head[i].n_pad;
+    hmax = hb > hmax ? hb : hmax;
+  }
+  L->head0 = off;
+  off += align_up(hmax);
+  L->head1 = off;
+  off += align_up(hmax);
+  L->total = off;
+  return XPG_OK;
+}
+
+int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t ldw, int64_t k_pad,
+                 const float* bias, int64_t n_real, int64_t n_pad, int act, float* C, int64_t ldc,
+                 hipStream_t st) {
+  XPG_REQ(k_pad % 8 == 0 && n_pad % 32 == 0 && n_pad >= 32 && n_pad <= 256,
+          "xpg_dense: k_pad % 8, n_pad in {32..256} step 32 required");
+  XPG_REQ(lda % 4 == 0 && ldw % 4 == 0, "xpg_dense: lda/ldw must be multiples of 4");
+  if (M <= 0) return XPG_OK;
+  const int64_t waves = cdiv(M, 32);
+  dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
+  const int kp = static_cast<int>(k_pad), nr = static_cast<int>(n_real);
+  switch (n_pad / 32) {
+#define XPG_DENSE_CASE(NT) \
+    case NT: hipLaunchKernelGGL(k_dense<NT>, grid, block, 0, st, A, M, lda, W, ldw, kp, bias, nr, act, C, ldc); break;
+    XPG_DENSE_CASE(1) XPG_DENSE_CASE(2) XPG_DENSE_CASE(3) XPG_DENSE_CASE(4)
+    XPG_DENSE_CASE(5) XPG_DENSE_CASE(6) XPG_DENSE_CASE(7) XPG_DENSE_CASE(8)
+#undef XPG_DENSE_CASE
+    default: return fail(XPG_EINVAL, "xpg_dense: unsupported n_pad");
+  }
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+template <bool L1>
+int launch_agg(const AggArgs& a, hipStream_t st) {
+  XPG_REQ(a.width % 32 == 0 && a.width > 0, "agg: row width must be a positive multiple of 32");
+  const int f4 = a.width / 4;  // float4 chunks per row (>= 8)
+  const int lps = f4 >= 64 ? 64 : f4;
+  const int nv = f4 / lps;
+  XPG_REQ(f4 % lps == 0 && (nv == 1 || nv == 2 || nv == 4), "agg: unsupported row width");
+  const int64_t threads = a.rows * a.n_tgt * lps;
+  if (threads == 0) return XPG_OK;
+  dim3 grid(static_cast<unsigned>(cdiv(threads, 256))), block(256);
+#define XPG_AGG(LPS, NV) \
+  if (lps == LPS && nv == NV) { hipLaunchKernelGGL((k_agg<L1, LPS, NV>), grid, block, 0, st, a); XPG_LAUNCHED(); return XPG_OK; }
+  XPG_AGG(8, 1) XPG_AGG(16, 1) XPG_AGG(32, 1) XPG_AGG(64, 1) XPG_AGG(64, 2) XPG_AGG(64, 4)
+  // widths that are odd multiples of 32 below 256 (e.g. 96) map to lps = f4 (non power of 2)
+  XPG_AGG(24, 1) XPG_AGG(40, 1) XPG_AGG(48, 1) XPG_AGG(56, 1)
+#undef XPG_AGG
+  return fail(XPG_EINVAL, "agg: unsupported row width " + std::to_string(a.width));
+}
+
+}  // namespace
+
+// ==================================================================================== C-ABI
+extern "C" {
+
+int xpg_abi_version(void) { return XPG_ABI_VERSION; }
+
+const char* xpg_last_error(void) { return g_err.c_str(); }
+
+int xpg_pack_masks(const uint8_t* mask, int64_t rows, int64_t cols, uint32_t* bits, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 0, "pack: bad shape");
+  const int words = words_of(cols);
+  const int64_t n = rows * words;
+  if (n == 0) return XPG_OK;
+  hipLaunchKernelGGL(k_pack, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, S(stream), mask, rows, cols, words, bits);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+int xpg_unpack_masks(const uint32_t* bits, int64_t rows, int64_t cols, uint8_t* mask, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 0, "unpack: bad shape");
+  const int64_t n = rows * cols;
+  if (n == 0) return XPG_OK;
+  hipLaunchKernelGGL(k_unpack, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, S(stream), bits, rows, cols, words_of(cols), mask);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 0 && row_offset >= 0, "shapley: bad shape");
+  const int words = words_of(cols);
+  const int64_t n = rows * ((words + 3) / 4);
+  if (n == 0) return XPG_OK;
+  hipLaunchKernelGGL(k_shapley, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, S(stream), seed, row_offset, rows, cols, words, bits);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+int xpg_edge_keep(const uint32_t* bits, int64_t rows, int64_t cols, const int32_t* src, const int32_t* dst,
+                  int64_t n_edges, uint8_t* keep, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 0 && n_edges >= 0, "edge_keep: bad shape");
+  const int64_t n = rows * n_edges;
+  if (n == 0) return XPG_OK;
+  hipLaunchKernelGGL(k_edge_keep, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, S(stream), bits, rows, words_of(cols), src, dst, n_edges, keep);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+int xpg_popcount_rows(const uint32_t* bits, int64_t rows, int64_t cols, int32_t* counts, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 0, "popcount: bad shape");
+  if (rows == 0) return XPG_OK;
+  hipLaunchKernelGGL(k_popcount, dim3(static_cast<unsigned>(cdiv(rows, 4))), dim3(256), 0, S(stream), bits, rows, words_of(cols), counts);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+int xpg_shap_kernel(const int32_t* counts, int64_t rows, int64_t cols, double* kernel_out, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 1, "shap_kernel: need cols > 1");
+  if (rows == 0) return XPG_OK;
+  hipLaunchKernelGGL(k_shap, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+int xpg_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t ldw, int64_t k_pad, const float* bias,
+              int64_t n_real, int64_t n_pad, int act, float* C, int64_t ldc, xpg_stream_t stream) {
+  return launch_dense(A, M, lda, W, ldw, k_pad, bias, n_real, n_pad, act, C, ldc, S(stream));
+}
+
+int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* bytes) {
+  WsLayout L;
+  int rc = layout_ws(plan, rows, &L);
+  if (rc) return rc;
+  *bytes = L.total;
+  return XPG_OK;
+}
+
+int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y,
+                       void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
+  WsLayout L;
+  int rc = layout_ws(p, rows, &L);
+  if (rc) return rc;
+  XPG_REQ(workspace_bytes >= L.total, "masked_forward: workspace too small");
+  XPG_REQ(p->n_rel >= 1 && p->n0 >= 1 && p->cols > 0, "masked_forward: bad plan sizes");
+  if (rows == 0) return XPG_OK;
+  hipStream_t st = S(stream);
+  char* ws = static_cast<char*>(workspace);
+  float* kin = reinterpret_cast<float*>(ws + L.kin);
+  const int words = words_of(p->cols);
+  {
+    const int64_t n = rows * (int64_t)p->n_rel * p->n0;
+    hipLaunchKernelGGL(k_degree, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, st, bits, rows, words, p->n0,
+                       p->n_rel, p->f0_node, p->deg_ptr, p->deg_src, kin);
+    XPG_LAUNCHED();
+  }
+  for (int l = 0; l < p->n_layers; ++l) {
+    const xpg_layer_desc& ly = p->layers[l];
+    XPG_REQ(ly.n_terms >= 1 && ly.n_terms <= XPG_MAX_TERMS, "layer: 1..8 terms");
+    AggArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.rows = rows;
+    a.n0 = p->n0;
+    a.n_rel = p->n_rel;
+    a.n_tgt = ly.n_tgt;
+    a.n_prev = l == 0 ? p->n0 : p->layers[l - 1].n_tgt;
+    a.kin = kin;
+    a.tgt_prev = ly.tgt_prev;
+    a.tgt_f0 = ly.tgt_f0;
+    a.agg_ptr = ly.agg_ptr;
+    a.agg_src = ly.agg_src;
+    a.agg_f0 = ly.agg_f0;
+    a.self_mult = ly.self_mult;
+    a.n_terms = ly.n_terms;
+    for (int k = 0; k < ly.n_terms; ++k) {
+      a.kind[k] = ly.terms[k].kind;
+      a.rel[k] = ly.terms[k].rel;
+      a.table[k] = ly.terms[k].table;
+      XPG_REQ(a.kind[k] == XPG_TERM_ROOT || (a.rel[k] >= 0 && a.rel[k] < p->n_rel), "term: bad relation");
+    }
+    float* hout = reinterpret_cast<float*>(ws + L.h[l]);
+    if (l == 0) {
+      a.width = ly.f_out_pad;
+      a.out = hout;
+      a.out_ld = ly.f_out_pad;
+      a.bias = ly.bias;
+      a.act = ly.act;
+      a.f_real = ly.f_out;
+      rc = launch_agg<true>(a, st);
+      if (rc) return rc;
+    } else {
+      const xpg_layer_desc& prev = p->layers[l - 1];
+      XPG_REQ(ly.f_in_pad == prev.f_out_pad, "layer: f_in_pad must equal previous f_out_pad");
+      float* agg = reinterpret_cast<float*>(ws + L.agg);
+      a.hprev = reinterpret_cast<const float*>(ws + L.h[l - 1]);
+      a.width = ly.f_in_pad;
+      a.out = agg;
+      a.out_ld = (int64_t)ly.n_terms * ly.f_in_pad;
+      rc = launch_agg<false>(a, st);
+      if (rc) return rc;
+      rc = launch_dense(agg, rows * ly.n_tgt, a.out_ld, ly.weight, a.out_ld, a.out_ld, ly.bias, ly.f_out,
+                        ly.f_out_pad, ly.act, hout, ly.f_out_pad, st);
+      if (rc) return rc;
+    }
+  }
+  const xpg_layer_desc& last = p->layers[p->n_layers - 1];
+  const int64_t M = rows * last.n_tgt;
+  const float* cur = reinterpret_cast<const float*>(ws + L.h[p->n_layers - 1]);
+  int64_t cur_ld = last.f_out_pad;
+  for (int i = 0; i < p->n_head; ++i) {
+    const xpg_head_desc& hd = p->head[i];
+    XPG_REQ(hd.k_pad == cur_ld, "head: k_pad must equal the previous padded width");
+    float* nxt = reinterpret_cast<float*>(ws + ((i & 1) ? L.head1 : L.head0));
+    rc = launch_dense(cur, M, cur_ld, hd.weight, hd.k_pad, hd.k_pad, hd.bias, hd.n_real, hd.n_pad, hd.act, nxt,
+                      hd.n_pad, st);
+    if (rc) return rc;
+    cur = nxt;
+    cur_ld = hd.n_pad;
+  }
+  hipLaunchKernelGGL(k_take_col, dim3(static_cast<unsigned>(cdiv(M, 256))), dim3(256), 0, st, cur, M, cur_ld,
+                     p->out_col, y);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch, const float* y,
+                const double* kernel, const xpg_wlm_params* params, int64_t step0, float* w,
+                float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, xpg_stream_t stream) {
+  XPG_REQ(rows > 0 && cols > 0 && batch > 0 && params, "wlm_fit: bad arguments");
+  const int words = words_of(cols);
+  const int64_t pitch = ((batch + 3) & ~int64_t(3)) + 4 * ((((batch + 3) / 4) & 1) == 0);  // odd # of 16B slots
+  const size_t lds = 256 + sizeof(float) * (((size_t)words * 33 + 3) & ~size_t(3)) +
+                     sizeof(float) * 2 * pitch + sizeof(uint32_t) * (size_t)words * pitch;
+  XPG_REQ(lds <= 160 * 1024, "wlm_fit: batch x columns too large for the single-workgroup fit (LDS)");
+  XPG_REQ(cols <= 16 * 1024, "wlm_fit: more than 16384 columns not supported by the single-workgroup fit");
+  const int cpt = static_cast<int>(cdiv(cols, 1024));
+  hipStream_t st = S(stream);
+  const int ic = static_cast<int>(cols), ib = static_cast<int>(batch), ip = static_cast<int>(pitch);
+#define XPG_WLM(C)                                                                                          \
+  if (cpt <= C) {                                                                                           \
+    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm<C>),                                   \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));        \
+    hipLaunchKernelGGL(k_wlm<C>, dim3(1), dim3(1024), lds, st, bits, rows, ic, words, ib, ip, y, kernel,    \
+                       *params, step0, w, adam_m, adam_v, losses, best_epoch);                              \
+    XPG_LAUNCHED();                                                                                         \
+    return XPG_OK;                                                                                          \
+  }
+  XPG_WLM(1) XPG_WLM(2) XPG_WLM(4) XPG_WLM(8) XPG_WLM(16)
+#undef XPG_WLM
+  return fail(XPG_EINVAL, "wlm_fit: unsupported column count");
+}
+
+}  // extern "C"

@@ -1,0 +1,322 @@
+"""Device engine: builds receptive-field plans and drives the HIP kernels (libxpgnn.so).
+
+Plan (per query, built once per Explainer.run — DESIGN.md §3):
+  F_L = queries; F_{l-1} = F_l ∪ in-neighbours(F_l) (all relations), F_l first so the first
+  n_l entries of F_{l-1} are F_l.  Degrees are needed at F_0 (their in-edges reach hop L+1,
+  which is why the reference extracts L+1 hops, data.py:325-328).
+  Layer-1 tables T_k = X[F_0] W_k^T are computed once by the MFMA dense kernel (features are
+  never masked, data.py:582); per mask row only the masked aggregation and the deeper layers
+  (aggregate-then-transform on MFMA) run.
+
+All device memory is owned by torch tensors held by the plan; the C-ABI never allocates.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import ACT, TERM, ForwardPlanDesc, HeadDesc, LayerDesc, WlmParams, call, ptr
+
+
+def _rup(x, m):
+    return ((int(x) + m - 1) // m) * m
+
+
+def words_of(cols):
+    return (int(cols) + 31) // 32
+
+
+# ----------------------------------------------------------------------------- masks
+def pack_masks(mask: torch.Tensor) -> torch.Tensor:
+    """bool/uint8 [rows, cols] device tensor -> row bits uint32 [rows, words] (HIP)."""
+    _lib.require_device(mask, "mask")
+    m = mask.contiguous()
+    if m.dtype == torch.bool:
+        m = m.view(torch.uint8)
+    rows, cols = m.shape
+    bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=m.device)
+    call("xpg_pack_masks", ptr(m), rows, cols, ptr(bits), _lib.stream_of(m.device))
+    return bits
+
+
+def unpack_masks(bits: torch.Tensor, cols: int) -> torch.Tensor:
+    _lib.require_device(bits, "bits")
+    rows = bits.shape[0]
+    out = torch.empty((rows, cols), dtype=torch.uint8, device=bits.device)
+    call("xpg_unpack_masks", ptr(bits), rows, cols, ptr(out), _lib.stream_of(bits.device))
+    return out.view(torch.bool)
+
+
+def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0):
+    """Device Shapley masks (masks.py:231-260 distribution: iid Bernoulli(1/2) bits)."""
+    bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=device)
+    call("xpg_sample_shapley", ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), row_offset, rows,
+         cols, ptr(bits), _lib.stream_of(torch.device(device)))
+    return bits
+
+
+def edge_keep(bits, cols, src, dst):
+    """data.py:390-451 edge mask: [rows * n_edges] bool, copy-major."""
+    _lib.require_device(bits, "bits")
+    rows = bits.shape[0]
+    s = src.to(device=bits.device, dtype=torch.int32).contiguous()
+    d = dst.to(device=bits.device, dtype=torch.int32).contiguous()
+    keep = torch.empty(rows * s.numel(), dtype=torch.uint8, device=bits.device)
+    call("xpg_edge_keep", ptr(bits), rows, cols, ptr(s), ptr(d), s.numel(), ptr(keep),
+         _lib.stream_of(bits.device))
+    return keep.view(torch.bool)
+
+
+# ----------------------------------------------------------------------------- KernelSHAP
+def shap_kernel(bits: torch.Tensor, cols: int) -> torch.Tensor:
+    """Kernel.compute (kernels.py:115-174) on device: fp64 [rows]."""
+    _lib.require_device(bits, "bits")
+    rows = bits.shape[0]
+    counts = torch.empty(rows, dtype=torch.int32, device=bits.device)
+    out = torch.empty(rows, dtype=torch.float64, device=bits.device)
+    st = _lib.stream_of(bits.device)
+    call("xpg_popcount_rows", ptr(bits), rows, cols, ptr(counts), st)
+    call("xpg_shap_kernel", ptr(counts), rows, cols, ptr(out), st)
+    return out
+
+
+# ----------------------------------------------------------------------------- dense
+def dense(A: torch.Tensor, W: torch.Tensor, bias, act=None, n_real=None) -> torch.Tensor:
+    """act(A W^T + b) on the fp32 MFMA kernel.  A [M, K] and W [N, K] are zero-padded here."""
+    dev = A.device
+    M, K = A.shape
+    N = W.shape[0] if n_real is None else n_real
+    k_pad, n_pad = _rup(K, 8), _rup(max(N, 1), 32)
+    Ap = A if (K == k_pad and A.is_contiguous()) else \
+        torch.nn.functional.pad(A.float(), (0, k_pad - K)).contiguous()
+    Wp = torch.zeros((n_pad, k_pad), dtype=torch.float32, device=dev)
+    Wp[:W.shape[0], :K] = W
+    bp = torch.zeros(n_pad, dtype=torch.float32, device=dev)
+    if bias is not None:
+        bp[:bias.shape[0]] = bias
+    C = torch.empty((M, n_pad), dtype=torch.float32, device=dev)
+    call("xpg_dense", ptr(Ap), M, k_pad, ptr(Wp), k_pad, k_pad, ptr(bp), N, n_pad,
+         ACT[act], ptr(C), n_pad, _lib.stream_of(dev))
+    return C[:, :N]
+
+
+# ----------------------------------------------------------------------------- forward plan
+def plan_arrays(S, rel_np, queries, L):
+    """Receptive-field frontiers and CSR arrays (numpy; see include/xpgnn.h).
+
+    frontiers[L] = queries; frontiers[l-1] = frontiers[l] + sorted new in-neighbours (all
+    relations), so frontiers[l] is a prefix of frontiers[l-1].  deg_*: in-edges (self-loops
+    excluded) of every F_0 node per relation, relation-major with absolute offsets.  layers[l-1]:
+    in-edges of F_l targets (self-loops excluded) with source positions in F_{l-1} and F_0, plus
+    the multiplicity of (t, t) edges per relation."""
+    all_src = np.concatenate([e[0] for e in rel_np]) if rel_np else np.zeros(0, np.int64)
+    all_dst = np.concatenate([e[1] for e in rel_np]) if rel_np else np.zeros(0, np.int64)
+    fr = [None] * (L + 1)
+    fr[L] = np.asarray(queries, dtype=np.int64).reshape(-1)
+    if fr[L].size == 0 or fr[L].min() < 0 or fr[L].max() >= S:
+        raise ValueError("query positions out of range")
+    if np.unique(fr[L]).size != fr[L].size:
+        raise ValueError("duplicate query positions")
+    for lvl in range(L, 0, -1):
+        cur = fr[lvl]
+        mark = np.zeros(S, dtype=bool)
+        mark[cur] = True
+        nb = np.unique(all_src[mark[all_dst]])
+        fr[lvl - 1] = np.concatenate([cur, nb[~mark[nb]]])
+    pos = []
+    for lvl in range(L + 1):
+        p = np.full(S, -1, dtype=np.int64)
+        p[fr[lvl]] = np.arange(fr[lvl].size)
+        pos.append(p)
+    n0 = fr[0].size
+
+    def csr(targets_pos, n_t, src_pos_maps):
+        ptrs, cols, off = [], [[] for _ in src_pos_maps], 0
+        smul = []
+        for s, d in rel_np:
+            k = s != d
+            s2, d2 = s[k], d[k]
+            sel = targets_pos[d2] >= 0
+            key = targets_pos[d2[sel]]
+            order = np.argsort(key, kind="stable")
+            src_nodes = s2[sel][order]
+            for j, m in enumerate(src_pos_maps):
+                cols[j].append(m(src_nodes))
+            cnt = np.bincount(key, minlength=n_t)
+            ptrs.append(np.concatenate([[0], np.cumsum(cnt)]) + off)
+            off += int(cnt.sum())
+            loops = s[~k]
+            ls = targets_pos[loops] >= 0
+            smul.append(np.bincount(targets_pos[loops[ls]], minlength=n_t))
+        cat = [np.concatenate(c) if c else np.zeros(0, np.int64) for c in cols]
+        return np.concatenate(ptrs), cat, np.concatenate(smul)
+
+    deg_ptr, (deg_src,), _ = csr(pos[0], n0, [lambda v: v])
+    layers = []
+    for lvl in range(1, L + 1):
+        ptr_, (a_src, a_f0), smul = csr(pos[lvl], fr[lvl].size,
+                                        [lambda v, l=lvl: pos[l - 1][v], lambda v: pos[0][v]])
+        layers.append({"agg_ptr": ptr_, "agg_src": a_src, "agg_f0": a_f0, "self_mult": smul})
+    return {"frontiers": fr, "pos": pos, "deg_ptr": deg_ptr, "deg_src": deg_src,
+            "layers": layers}
+
+
+class ForwardPlan:
+    """Receptive-field plan of one (subgraph, model program, query set)."""
+
+    def __init__(self, program, sub_feat, rel_edges, queries, device=None):
+        device = torch.device(device) if device is not None else sub_feat.device
+        _lib.require_device(torch.empty(0, device=device), "plan device")
+        if len(program.convs) == 0:
+            raise ValueError("program has no conv layer")
+        self.device = device
+        self.program = program
+        self.cols = int(sub_feat.shape[0])
+        S = self.cols
+        self.n_rel = len(rel_edges)
+        self._keep = []  # device tensors referenced by descriptors
+
+        rel_np = [np.asarray(e.detach().cpu().numpy(), dtype=np.int64).reshape(2, -1)
+                  for e in rel_edges]
+        L = len(program.convs)
+        arr = plan_arrays(S, rel_np, queries, L)
+        self.arrays = arr
+        fr = arr["frontiers"]
+        n0 = fr[0].size
+        self.n0 = n0
+        self.frontiers = fr
+        self._deg_ptr = self._i32(arr["deg_ptr"])
+        self._deg_src = self._i32(arr["deg_src"] if arr["deg_src"].size else np.zeros(1))
+        self._f0_node = self._i32(fr[0])
+
+        X0 = sub_feat.to(device=device, dtype=torch.float32)[torch.as_tensor(fr[0], device=device)]
+        f_in0 = program.convs[0].f_in
+        if X0.shape[1] != f_in0:
+            raise ValueError(f"feature width {X0.shape[1]} != first conv input {f_in0}")
+
+        self._layers = (LayerDesc * L)()
+        prev_pad = None
+        for li, conv in enumerate(program.convs):
+            lvl = li + 1
+            n_t = fr[lvl].size
+            f_out_pad = _rup(conv.f_out, 32)
+            if f_out_pad > 256 or len(conv.terms) > _lib.MAX_TERMS:
+                raise ValueError("conv wider than 256 or more than 8 terms is not supported")
+            ld = self._layers[li]
+            ld.n_terms = len(conv.terms)
+            ld.act = ACT[conv.act]
+            ld.f_out = conv.f_out
+            ld.f_out_pad = f_out_pad
+            ld.n_tgt = n_t
+            ld.f_in_pad = 0 if li == 0 else prev_pad
+            ld.tgt_prev = self._i32(np.arange(n_t)).data_ptr()  # F_l is a prefix of F_{l-1}
+            ld.tgt_f0 = self._i32(arr["pos"][0][fr[lvl]]).data_ptr()
+            lay = arr["layers"][li]
+            ld.agg_ptr = self._i32(lay["agg_ptr"]).data_ptr()
+            ld.agg_src = self._i32(lay["agg_src"] if lay["agg_src"].size else np.zeros(1)).data_ptr()
+            ld.agg_f0 = self._i32(lay["agg_f0"] if lay["agg_f0"].size else np.zeros(1)).data_ptr()
+            ld.self_mult = self._i32(lay["self_mult"]).data_ptr()
+            bias = torch.zeros(f_out_pad, dtype=torch.float32, device=device)
+            bias[:conv.f_out] = conv.bias.to(device)
+            self._keep.append(bias)
+            ld.bias = bias.data_ptr()
+            for k, term in enumerate(conv.terms):
+                ld.terms[k].kind = TERM[term.kind]
+                ld.terms[k].rel = term.rel
+            if li == 0:
+                for k, term in enumerate(conv.terms):
+                    T = dense(X0, term.weight.to(device), None, None)
+                    Tp = torch.zeros((n0, f_out_pad), dtype=torch.float32, device=device)
+                    Tp[:, :conv.f_out] = T
+                    self._keep.append(Tp)
+                    ld.terms[k].table = Tp.data_ptr()
+                ld.weight = None
+            else:
+                kt = len(conv.terms) * prev_pad
+                Wc = torch.zeros((f_out_pad, kt), dtype=torch.float32, device=device)
+                for k, term in enumerate(conv.terms):
+                    Wc[:conv.f_out, k * prev_pad:k * prev_pad + conv.f_in] = term.weight.to(device)
+                self._keep.append(Wc)
+                ld.weight = Wc.data_ptr()
+            prev_pad = f_out_pad
+
+        self._head = (HeadDesc * max(1, len(program.head)))()
+        for i, h in enumerate(program.head):
+            n_real, k_real = h.weight.shape
+            n_pad = _rup(n_real, 32)
+            if n_pad > 256:
+                raise ValueError("head layer wider than 256 is not supported")
+            Wp = torch.zeros((n_pad, prev_pad), dtype=torch.float32, device=device)
+            Wp[:n_real, :k_real] = h.weight.to(device)
+            bp = torch.zeros(n_pad, dtype=torch.float32, device=device)
+            if h.bias is not None:
+                bp[:n_real] = h.bias.to(device)
+            self._keep += [Wp, bp]
+            hd = self._head[i]
+            hd.k_pad, hd.n_real, hd.n_pad, hd.act = prev_pad, n_real, n_pad, ACT[h.act]
+            hd.weight, hd.bias = Wp.data_ptr(), bp.data_ptr()
+            prev_pad = n_pad
+
+        self.n_out = fr[L].size
+        self.desc = ForwardPlanDesc(
+            cols=S, n_rel=self.n_rel, n0=n0, f0_node=self._f0_node.data_ptr(),
+            deg_ptr=self._deg_ptr.data_ptr(), deg_src=self._deg_src.data_ptr(), n_layers=L,
+            layers=self._layers, n_head=len(program.head), head=self._head,
+            out_col=program.out_col)
+        self._ws = None
+
+    def _i32(self, a):
+        t = torch.as_tensor(np.ascontiguousarray(a, dtype=np.int32), device=self.device)
+        self._keep.append(t)
+        return t
+
+    def workspace_bytes(self, rows):
+        n = ctypes.c_size_t(0)
+        _lib.check(_lib.load().xpg_forward_workspace(ctypes.byref(self.desc), rows, ctypes.byref(n)))
+        return n.value
+
+    def forward(self, bits: torch.Tensor, max_ws_bytes=8 << 30) -> torch.Tensor:
+        """y [rows, n_out] fp32: model output at each target of the last conv layer, per mask
+        row (wlm.py:349-436 for one batch, all batches at once)."""
+        _lib.require_device(bits, "bits")
+        rows = bits.shape[0]
+        y = torch.empty((rows, self.n_out), dtype=torch.float32, device=self.device)
+        if rows == 0:
+            return y
+        per_row = max(1, self.workspace_bytes(1))
+        chunk = max(1, min(rows, max_ws_bytes // per_row))
+        need = self.workspace_bytes(chunk)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        st = _lib.stream_of(self.device)
+        for r0 in range(0, rows, chunk):
+            n = min(chunk, rows - r0)
+            call("xpg_masked_forward", ctypes.byref(self.desc), ptr(bits[r0:r0 + n]), n,
+                 ptr(y[r0:r0 + n]), ptr(self._ws), self._ws.numel(), st)
+        return y
+
+
+# ----------------------------------------------------------------------------- surrogate
+def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0):
+    """train_model (wlm.py:132-278) epoch loop on device.  Returns (w, losses, best_epoch,
+    adam_m, adam_v)."""
+    dev = bits.device
+    rows = bits.shape[0]
+    if batch <= 0:
+        raise ValueError("batch_size should be a positive integer value, but got "
+                         f"batch_size={batch}")
+    nsteps = math.ceil(rows / batch)
+    w = w0.detach().to(device=dev, dtype=torch.float32).reshape(-1).clone()
+    m = torch.zeros(cols, dtype=torch.float32, device=dev) if m0 is None else m0.clone()
+    v = torch.zeros(cols, dtype=torch.float32, device=dev) if v0 is None else v0.clone()
+    losses = torch.empty(nsteps, dtype=torch.float64, device=dev)
+    best = torch.empty(1, dtype=torch.int32, device=dev)
+    p = WlmParams(lr=abs(float(params["lr"])), l1_lambda=float(params["l1_lambda"]), beta1=0.9,
+                  beta2=0.999, eps=1e-8, weight_decay=1e-2)
+    yy = y.to(device=dev, dtype=torch.float32).contiguous()
+    kk = kernel.to(device=dev, dtype=torch.float64).contiguous()
+    call("xpg_wlm_fit", ptr(bits), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
+         int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), _lib.stream_of(dev))
+    return w, losses, best, m, v

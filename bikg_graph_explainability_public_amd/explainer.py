@@ -1,0 +1,241 @@
+"""`Explainer` — drop-in for pathway_explanations.explainer.Explainer (explainer.py:25-546).
+
+Same constructor, assertions and `run(element, times) -> (config_val_df, pathway_df)`.  The
+host orchestration (hetero flattening, computational subgraph, community filtering, output
+DataFrames) follows the reference step by step; the per-repeat hot path runs on the MI355X:
+
+  one ForwardPlan per query (receptive-field CSR + layer-1 tables, built once) ->
+  per repeat: masks -> bit-pack -> masked forward -> KernelSHAP -> surrogate Adam loop.
+
+Repeats draw masks and the surrogate's initial weights from torch's CPU generator in the
+reference's order (compat sampler), so results match the reference CPU path for the same seed.
+"""
+import random
+import warnings
+
+import numpy as np
+import torch
+
+from . import _lib, engine, pipeline
+from .data import Data
+from .masks import Mask, dataloader_seed_draw
+from .model import Model
+from .pathways import Pathways
+from .wlm import LinearRegression
+
+
+def set_seed(seed=100):
+    """explainer.py:14-22."""
+    random.seed(seed)
+    np.random.seed(seed + 1)
+    torch.manual_seed(seed + 2)
+    torch.cuda.manual_seed(seed + 3)
+    torch.cuda.manual_seed_all(seed + 4)
+    torch.backends.cudnn.enabled = False
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
+
+
+class Explainer:
+    def __init__(self, feat, edge_index, arch, params, names, pathways=None, pathway_names=None,
+                 element_type=None, problem="node_prediction", node_types=None,
+                 edge_types=None):
+        self.initial_assertions(feat, edge_index, arch, params, names, pathways, pathway_names,
+                                element_type, problem)
+        self.feat = feat
+        self.edge_index = edge_index
+        self.arch = arch
+        self.params = params
+        self.names = names
+        self.pathways = pathways
+        self.pathway_names = pathway_names
+        self.element_type = element_type
+        self.problem = problem.lower().strip()
+        self.node_types = node_types
+        self.edge_types = edge_types
+        self.last_run = None  # diagnostics of the last run (per-repeat losses, path used)
+
+    @staticmethod
+    def initial_assertions(feat, edge_index, arch, params, names, pathways, pathway_names,
+                           element_type, problem):
+        """explainer.py:106-189 (same messages)."""
+        if pathways is not None:
+            assert isinstance(pathways, (list, dict)), "Pathways is not list or dict"
+        if pathway_names is not None:
+            assert isinstance(pathway_names, (list, dict)), "Pathway names is not list or dict"
+            assert len(pathway_names) == len(pathways), \
+                "Length of list with pathway names and list with pathway indexes do not match"
+        assert isinstance(feat, (torch.Tensor, dict)), \
+            "Feature matrix is not torch tensor or dict"
+        assert isinstance(edge_index, (torch.Tensor, dict)), \
+            "Edge index matrix is not torch tensor or dict"
+        assert isinstance(names, (list, dict)), "Element names is not list or dict"
+        assert isinstance(params, dict), "Hyperparameters given is not dictionary"
+        assert isinstance(problem, str), "Problem type given is not string"
+        if element_type is not None:
+            assert isinstance(element_type, (str, tuple)), \
+                "Element type is not string (node) nor tuple (edge)"
+            if "node" in problem:
+                assert isinstance(feat, dict), "Feature given is not a dict of node types"
+                assert element_type in list(feat.keys()), \
+                    "Node type '{}' is not among input node types in heterogeneous graph" \
+                    .format(element_type)
+            elif "edge" in problem:
+                assert isinstance(edge_index, dict), \
+                    "Edge index given is not a dict of edge index types"
+                assert element_type in list(edge_index.keys()), \
+                    "Edge type '{}' is not among input node types in heterogeneous graph" \
+                    .format(element_type)
+
+    @staticmethod
+    def extract_index(element, names=None):
+        """explainer.py:191-226."""
+        if names is None:
+            assert isinstance(element, (int, float)), \
+                "No element names have been given and the node name given is not numeric"
+            return int(element)
+        assert element in names, "Element name '{}' is not present in the graph".format(element)
+        return int(np.where(np.array(names, dtype=str) == element)[0][0])
+
+    def filter_hetero_names(self, names, node_type, edge_type, node_type_names,
+                            edge_type_names):
+        """explainer.py:228-286."""
+        arr = np.array(names, dtype=str)
+        if isinstance(self.element_type, str):
+            idx = torch.where(node_type == node_type_names.index(self.element_type))[0]
+        elif isinstance(self.element_type, tuple):
+            idx = torch.where(edge_type == edge_type_names.index(self.element_type))[0]
+        else:
+            idx = torch.where(node_type == 1)[0]
+        return arr[idx.cpu().numpy()].tolist()
+
+    @staticmethod
+    def weight_stacking(weights):
+        """explainer.py:288-314 — mean and population std over repeats."""
+        stack = torch.vstack(weights)
+        return torch.mean(stack, 0), torch.std(stack, 0, unbiased=False)
+
+    # ------------------------------------------------------------------------------ run
+    def prepare(self, element, device):
+        """Host orchestration of explainer.py:345-480 (no RNG consumed): heterogeneous
+        flattening, computational subgraph, community filtering.  Returns a dict context."""
+        feat, ei = _to_device(self.feat, device), _to_device(self.edge_index, device)
+        raw = Data(feat, ei)
+        pw_raw = Pathways(self.pathways, self.pathway_names) if self.pathways is not None else None
+        (h_ntypes, h_etypes, feat, ei, node_types, edge_types, node_ptrs, edge_ptrs,
+         padded_dims) = raw.preprocess_hetero_graph()
+        if node_types is None and self.node_types is not None:
+            node_types = self.node_types.clone().to(device)
+        if edge_types is None and self.edge_types is not None:
+            edge_types = self.edge_types.clone().to(device)
+        names, _ = raw.hetero2homo_names(self.names)
+        pathways = pathway_names = pathway_types = None
+        if pw_raw is not None:
+            pathways, pathway_names, pathway_types = pw_raw.hetero2homo(self.problem, node_ptrs,
+                                                                       edge_ptrs)
+        data = Data(feat, ei)
+        sub_pw = sub_pw_names = None
+        sub_nt = sub_et = None
+        if "graph" not in self.problem:
+            rels = len(h_etypes) if h_etypes is not None else 0
+            n_hops = Model(self.arch).get_hops(rels)
+            ind = self.extract_index(element, names)
+            sub_feat, sub_ei, sub_names, sub_ind, sub_nt, sub_et = data.comp_graph(
+                ind, n_hops, self.problem, names, node_types, edge_types)
+            if pathways is not None:
+                sub_pw, sub_pw_names, _ = Pathways(pathways, pathway_names,
+                                                   pathway_types).comp_graph(sub_names)
+        else:
+            sub_feat, sub_ei, sub_names = feat.clone(), ei.clone(), names
+            sub_ind = self.extract_index(element, sub_names)
+            sub_nt = node_types.clone() if node_types is not None else None
+            sub_et = edge_types.clone() if edge_types is not None else None
+            if pathways is not None:
+                sub_pw, sub_pw_names = pathways, pathway_names
+        if "graph" not in self.problem and (self.element_type is not None or
+                                            self.node_types is not None or
+                                            self.edge_types is not None):
+            filt = self.filter_hetero_names(sub_names, sub_nt, sub_et, h_ntypes, h_etypes)
+            sub_ind = self.extract_index(element, filt)
+        sub_pw_inds = None
+        if pathways is not None:
+            spc = Pathways(sub_pw, sub_pw_names)
+            if isinstance(sub_pw[0][0], str):
+                sub_pw_inds = spc.names2inds(sub_names)
+            elif isinstance(sub_pw[0][0], int):
+                sub_pw_inds = sub_pw
+        if isinstance(sub_ind, torch.Tensor):
+            sub_ind = int(sub_ind.reshape(-1)[0])
+        S = Data(sub_feat, sub_ei).element_size(self.problem)
+        return {"sub_feat": sub_feat, "sub_ei": sub_ei, "sub_names": sub_names,
+                "sub_ind": sub_ind, "sub_nt": sub_nt, "sub_et": sub_et, "h_ntypes": h_ntypes,
+                "h_etypes": h_etypes, "padded_dims": padded_dims, "sub_pw": sub_pw,
+                "sub_pw_names": sub_pw_names, "sub_pw_inds": sub_pw_inds, "S": S,
+                "has_pathways": pathways is not None}
+
+    def run(self, element, times=1):
+        """explainer.py:316-546."""
+        if not torch.cuda.is_available():
+            raise _lib.NativeLibraryError("Explainer.run needs an MI355X (HIP) device; "
+                                          "there is no CPU fallback")
+        _lib.load()
+        device = torch.device("cuda", torch.cuda.current_device())
+        if times == 1:
+            set_seed(self.params["seed"])
+        c = self.prepare(element, device)
+        sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
+        geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
+
+        plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, [sub_ind], *geo)
+        if plan is not None and self.params.get("verify_arch", True):
+            ok, err = pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo)
+            if not ok:
+                warnings.warn(f"compiled arch disagrees with its torch forward (max err {err:.3g});"
+                              " using the generic torch path")
+                plan = None
+
+        sampler = self.params.get("mask_sampler", "compat")
+        _, epochs = Mask.assertions_mask_generator(self.params)
+        config_vals, diag = [], []
+        for _ in range(times):
+            if sampler == "device" and c["sub_pw_inds"] is None and "edge" not in self.problem:
+                R = int(self.params["interpret_samples"] * epochs)
+                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+                bits = engine.sample_shapley(seed, R, S, device)
+                mask = None
+            else:
+                mask, _ = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,
+                               self.problem).generate()
+                mask = mask.to(device)
+                bits = engine.pack_masks(mask)
+                R = mask.shape[0]
+            wlrm = LinearRegression(S)
+            dataloader_seed_draw()
+            batch = R // epochs
+            if plan is not None:
+                y = plan.forward(bits)[:, 0]
+            else:
+                if mask is None:
+                    mask = engine.unpack_masks(bits, S)
+                y = pipeline.generic_outputs(self.arch, sub_feat, sub_ei, mask, sub_ind,
+                                             self.problem, *geo, batch=batch)
+            w, losses, best, _ = pipeline.fit_repeat(bits, S, batch, y,
+                                                     wlrm.layer.weight.detach(), self.params)
+            config_vals.append(w)
+            diag.append({"losses": losses, "best_epoch": best, "rows": R, "batch": batch,
+                         "y": y, "bits": bits})
+        mean, std = self.weight_stacking(config_vals)
+        config_val_df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
+        pathway_df = None
+        if c["has_pathways"]:
+            pathway_df = Pathways(c["sub_pw"], c["sub_pw_names"]).aggregate(mean,
+                                                                            c["sub_pw_inds"])
+        self.last_run = {"engine": plan is not None, "repeats": diag, "S": S,
+                         "sub_ind": sub_ind, "plan": plan, "weights": config_vals}
+        return config_val_df, pathway_df
+
+
+def _to_device(x, device):
+    if isinstance(x, dict):
+        return {k: v.to(device) for k, v in x.items()}
+    return x.to(device)

@@ -1,0 +1,143 @@
+"""Perturbation masks: the reference's `Mask` class (masks.py:10-397) plus the device sampler.
+
+Two samplers share one output contract (bool [R, S] rows + per-row community index):
+
+* compat (default, `params["mask_sampler"] = "compat"`): restates masks.py:262-397 with torch's
+  CPU generator in the reference's exact call order — per community in length-descending order:
+  internal randint, external antithetic randint (+ extra row), optional dead-mask randperm; then
+  the row shuffle randperm — so masks are bit-identical to the reference CPU path for the same
+  RNG state (tests/test_masks_golden.py).  Rows are then bit-packed on the device.
+* device (`"device"`): counter-based Philox Shapley bits generated directly in HBM by the HIP
+  sampler (engine.sample_shapley) — same distribution, no host work; used for throughput.
+"""
+import itertools
+import math
+
+import torch
+from torch.utils.data import DataLoader
+
+from .data import Data
+from .pathways import Pathways
+
+
+def dataloader_seed_draw():
+    """The reference iterates its mask DataLoader once per repeat (wlm.py:210); creating the
+    iterator draws a base seed from torch's global CPU generator
+    (torch.utils.data.dataloader._BaseDataLoaderIter.__init__).  Compat mode replays that
+    draw so the next repeat's masks stay on the reference's random stream."""
+    torch.empty((), dtype=torch.int64).random_()
+
+
+class Mask(Data):
+    def __init__(self, feat, edge_index, pathways, params, problem):
+        super().__init__(feat, edge_index)
+        self.pathways = pathways
+        self.params = params
+        self.problem = problem
+
+    @staticmethod
+    def assertions_mask_generator(params):
+        """masks.py:37-60."""
+        n_perturbs = params["interpret_samples"]
+        epochs = params["epochs"]
+        assert isinstance(n_perturbs, (int, float)), \
+            "Number of perturbations in batch is not numeric"
+        assert isinstance(epochs, (int, float)), "Number of epochs in batch is not numeric"
+        return abs(n_perturbs), abs(epochs)
+
+    def obtain_device(self):
+        """masks.py:62-78."""
+        if isinstance(self.feat, dict):
+            return self.feat[list(self.feat.keys())[0]].device
+        return self.feat.device
+
+    @staticmethod
+    def get_internal_mask(pathway, len_pathways, total_size, device):
+        """masks.py:81-136 — rows proportional to the community size; random member bits."""
+        fraction = len(pathway) / torch.sum(len_pathways)
+        size = math.ceil(fraction * total_size)
+        size_internal = math.ceil(fraction * size)
+        if size_internal < 3:
+            size_internal, size = 1, 2
+        internal = torch.randint(0, 2, (size, len(pathway)), dtype=torch.bool)
+        return internal.to(device), size_internal
+
+    def get_external_indices(self, full_mask, ind_pathway, size_internal):
+        """masks.py:138-194 — external coalitions for rows size_internal..end.  Column
+        `ind_pathway` (the position in length-sorted order, as the reference passes it) is
+        switched off in the community mask."""
+        pw = Pathways(self.pathways, None)
+        device = full_mask.device
+        pmask = pw.mask_generator((full_mask.shape[0] - size_internal) // 2, full_mask.shape[0],
+                                  size_internal, torch.device("cpu"))
+        pmask[:, ind_pathway] = False
+        if len(self.pathways) - 1 > 0 and pmask.sum() == 0:
+            pmask = pw.activate_dead_mask(pmask, ind_pathway)
+        element, members = pw.pathway_mask2node_mask(pmask)
+        rows = torch.where(element)[0] + size_internal
+        out = full_mask.cpu()
+        out[rows, members[element]] = True
+        return out.to(device)
+
+    @staticmethod
+    def mask_loader(mask, pieces):
+        """masks.py:197-229 — DataLoader with batch_size = rows // pieces."""
+        return DataLoader(mask, batch_size=mask.shape[0] // pieces, num_workers=0)
+
+    def shapley_mask(self, size, device):
+        """masks.py:231-260."""
+        return torch.randint(0, 2, size, dtype=torch.bool).to(device)
+
+    def element_count(self):
+        if "edge" in self.problem:
+            # masks.py:292-294 reads a non-existent attribute for edge problems; mirror it.
+            return self.edge_size.shape[1]
+        return self.feat.shape[0]
+
+    def generate(self):
+        """Compat sampler: (mask bool [R, S] on CPU, pathway_rows int32 [R] or None)."""
+        n_perturbs, epochs = self.assertions_mask_generator(self.params)
+        total = n_perturbs * epochs
+        S = self.element_count()
+        if self.pathways is not None:
+            lens = torch.tensor([len(p) for p in self.pathways])
+            order = torch.argsort(lens, descending=True)
+            blocks, rows_of, sizes_of = [], [], []
+            cumulative = 0
+            for e in range(order.shape[0]):
+                pathway = self.pathways[order[e]]
+                pathway.sort()  # the reference sorts the caller's lists in place
+                internal, size_internal = self.get_internal_mask(pathway, lens, total, "cpu")
+                block = torch.zeros((internal.shape[0], S), dtype=torch.bool)
+                block = self.get_external_indices(block, e, size_internal)
+                block[:, pathway] = internal
+                rows_of.append([int(order[e])] * block.shape[0])
+                sizes_of.append([len(pathway)] * block.shape[0])
+                blocks.append(block)
+                if cumulative > total and S > 4000:
+                    break
+                cumulative += block.shape[0]
+            mask = torch.cat(blocks, dim=0)
+            prow = torch.tensor(list(itertools.chain.from_iterable(rows_of)), dtype=torch.int)
+            psize = torch.tensor(list(itertools.chain.from_iterable(sizes_of)), dtype=torch.int)
+        else:
+            mask = self.shapley_mask((total, S), "cpu")
+            prow = psize = None
+        if S > 4000 and mask.shape[0] > total and self.pathways is not None:
+            ind = torch.argsort(psize, descending=True)[:total]
+        else:
+            ind = torch.randperm(mask.shape[0])
+        mask = mask[ind]
+        if prow is not None:
+            prow = prow[ind]
+        return mask, prow
+
+    def mask_generator(self):
+        """masks.py:262-397 — (DataLoader over the shuffled mask, pathway_rows)."""
+        _, epochs = self.assertions_mask_generator(self.params)
+        mask, prow = self.generate()
+        device = self.obtain_device()
+        mask = mask.to(device)
+        if prow is not None:
+            prow = prow.to(device)
+        return self.mask_loader(mask, epochs), prow

@@ -1,0 +1,159 @@
+/*
+ * xpgnn.h — C-ABI of the MI355X-native XP-GNN perturbation-scoring engine (libxpgnn.so).
+ *
+ * Every entry point is `extern "C"`, takes plain device pointers + sizes + a HIP stream
+ * (`xpg_stream_t`, NULL = legacy default stream) and returns an int status (XPG_OK = 0);
+ * `xpg_last_error()` returns a thread-local message for the last failure.  No entry point
+ * allocates, frees or synchronises: device memory (inputs, outputs, workspaces) is owned by the
+ * caller (PyTorch tensors in the Python host), so every call can be captured in a hipGraph.
+ *
+ * Mask bit layout ("row bits"): uint32 [rows][words], words = ceil(cols / 32); element c of
+ * row r is bit (c & 31) of word r*words + (c >> 5).  Bits past `cols` in the last word are 0.
+ *
+ * Reference interfaces replaced (paths relative to /root/reference/src/pathway_explanations):
+ *   xpg_pack_masks / xpg_unpack_masks  — bool mask batches handed between masks.py and
+ *                                        wlm.py (DataLoader batches, masks.py:197-229)
+ *   xpg_sample_shapley                 — Mask.shapley_mask           masks.py:231-260
+ *   xpg_edge_keep                      — Data.build_edge_mask        data.py:390-451
+ *   xpg_popcount_rows + xpg_shap_kernel— Kernel.compute             kernels.py:115-174
+ *   xpg_masked_forward                 — Data.perturbator + Model.infer + extract_node_edge_output
+ *                                        (wlm.py:349-436 -> data.py:591-648, model.py:62-116,
+ *                                        model.py:295-328) for GCNConv / SAGEConv / HeteroConv-sum
+ *                                        conv stacks with a dense head
+ *   xpg_dense                          — the dense feature x weight contraction inside each layer
+ *                                        (PyG Linear / GCNConv.lin / SAGEConv.lin_l|lin_r)
+ *   xpg_wlm_fit                        — train_model's epoch loop     wlm.py:132-278 with
+ *                                        LinearRegression, regularizer, weighted_mse_loss and
+ *                                        torch.optim.Adam(weight_decay=1e-2) (wlm.py:17-129,441-520)
+ */
+#ifndef XPGNN_H
+#define XPGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XPG_ABI_VERSION 1
+#define XPG_MAX_TERMS 8
+
+typedef void* xpg_stream_t; /* hipStream_t */
+
+enum xpg_status { XPG_OK = 0, XPG_EINVAL = 1, XPG_EHIP = 2, XPG_ENOSPC = 3 };
+
+enum xpg_act { XPG_ACT_NONE = 0, XPG_ACT_RELU = 1, XPG_ACT_SIGMOID = 2, XPG_ACT_TANH = 3,
+               XPG_ACT_LEAKY_RELU = 4, XPG_ACT_ELU = 5 };
+
+/* aggregation term kinds of one conv layer (one term per relation, plus ROOT for SAGE) */
+enum xpg_term { XPG_TERM_GCN = 0,   /* D^-1/2 (A_r + I) D^-1/2 over relation r               */
+                XPG_TERM_MEAN = 1,  /* mean over kept in-edges of relation r (SAGE aggr)      */
+                XPG_TERM_ROOT = 2   /* the target's own row (SAGE lin_r)                     */ };
+
+int xpg_abi_version(void);
+const char* xpg_last_error(void);
+
+/* ---------------------------------------------------------------- masks */
+int xpg_pack_masks(const uint8_t* mask, int64_t rows, int64_t cols, uint32_t* bits,
+                   xpg_stream_t stream);
+int xpg_unpack_masks(const uint32_t* bits, int64_t rows, int64_t cols, uint8_t* mask,
+                     xpg_stream_t stream);
+/* Shapley masks, P(bit) = 1/2, counter-based Philox4x32-10 keyed by (seed, global row). */
+int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
+                       uint32_t* bits, xpg_stream_t stream);
+
+/* ---------------------------------------------------------------- perturbation */
+/* keep[b*n_edges + e] = bit(b, src[e]) & bit(b, dst[e])   (data.py:420-449) */
+int xpg_edge_keep(const uint32_t* bits, int64_t rows, int64_t cols, const int32_t* src,
+                  const int32_t* dst, int64_t n_edges, uint8_t* keep, xpg_stream_t stream);
+
+/* ---------------------------------------------------------------- KernelSHAP */
+int xpg_popcount_rows(const uint32_t* bits, int64_t rows, int64_t cols, int32_t* counts,
+                      xpg_stream_t stream);
+/* kernel_out[r] from counts[r] with M = cols-1: exact formula for M <= 1000, the reference's
+ * ref-1000 approximation with its 0.9 back-off otherwise, then +-inf/NaN -> 0. */
+int xpg_shap_kernel(const int32_t* counts, int64_t rows, int64_t cols, double* kernel_out,
+                    xpg_stream_t stream);
+
+/* ---------------------------------------------------------------- dense (MFMA fp32) */
+/* C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) for n < n_real, 0 for n_real <= n < n_pad.
+ * k_pad % 8 == 0 (A and W zero-padded in k), n_pad % 32 == 0 (<= 256), W has n_pad rows,
+ * lda/ldw/ldc multiples of 4, pointers 16-byte aligned. */
+int xpg_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t ldw,
+              int64_t k_pad, const float* bias, int64_t n_real, int64_t n_pad, int act,
+              float* C, int64_t ldc, xpg_stream_t stream);
+
+/* ---------------------------------------------------------------- masked forward */
+/* Frontier formulation: F_L ⊆ ... ⊆ F_1 ⊆ F_0 are the subgraph nodes whose layer outputs are
+ * needed (the query's receptive field; or every node for a full-graph pass).  All CSR arrays
+ * are device pointers; per-relation CSRs are concatenated (ptr arrays hold absolute offsets,
+ * relation r's segment of a ptr array starts at r * (n + 1)). */
+typedef struct xpg_term_desc {
+  int32_t kind;            /* enum xpg_term                                             */
+  int32_t rel;             /* relation index (degree slot); ignored for ROOT           */
+  const float* table;      /* layer 1 only: pre-transformed F_0 rows [n0][f_out_pad]   */
+} xpg_term_desc;
+
+typedef struct xpg_layer_desc {
+  int32_t n_terms;
+  int32_t act;             /* activation after the conv (enum xpg_act)                 */
+  int32_t f_in_pad;        /* width of this layer's input rows (layer >= 2), % 8 == 0   */
+  int32_t f_out;           /* real output width                                        */
+  int32_t f_out_pad;       /* padded output width, % 32 == 0, <= 256                   */
+  int32_t n_tgt;           /* |F_l|                                                    */
+  const int32_t* tgt_prev; /* [n_tgt] position of each target inside F_{l-1}          */
+  const int32_t* tgt_f0;   /* [n_tgt] position of each target inside F_0               */
+  const int32_t* agg_ptr;  /* [n_rel * (n_tgt + 1)] in-edges per target, self-loops out */
+  const int32_t* agg_src;  /* source positions inside F_{l-1}                          */
+  const int32_t* agg_f0;   /* source positions inside F_0                              */
+  const int32_t* self_mult;/* [n_rel * n_tgt] multiplicity of (t, t) edges             */
+  xpg_term_desc terms[XPG_MAX_TERMS];
+  const float* weight;     /* layer >= 2: [f_out_pad][n_terms * f_in_pad]               */
+  const float* bias;       /* [f_out_pad], summed over relations, zero-padded          */
+} xpg_layer_desc;
+
+typedef struct xpg_head_desc {
+  int32_t k_pad, n_real, n_pad, act;
+  const float* weight;     /* [n_pad][k_pad], zero-padded                              */
+  const float* bias;       /* [n_pad], zero-padded                                     */
+} xpg_head_desc;
+
+typedef struct xpg_forward_plan {
+  int64_t cols;            /* mask columns S                                           */
+  int32_t n_rel;           /* relations (1 for homogeneous graphs)                     */
+  int32_t n0;              /* |F_0|                                                    */
+  const int32_t* f0_node;  /* [n0] subgraph node id of each F_0 position              */
+  const int32_t* deg_ptr;  /* [n_rel * (n0 + 1)] in-edges of F_0 nodes, self-loops out */
+  const int32_t* deg_src;  /* subgraph node ids                                        */
+  int32_t n_layers;
+  const xpg_layer_desc* layers;   /* host array [n_layers]                             */
+  int32_t n_head;
+  const xpg_head_desc* head;      /* host array [n_head]                               */
+  int32_t out_col;         /* output column extracted (0)                              */
+} xpg_forward_plan;
+
+/* Workspace needed by xpg_masked_forward for `rows` mask rows. */
+int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* bytes);
+/* y[r * n_last + i] = model output (column out_col) of target i of the last conv layer for
+ * mask row r (n_last = layers[n_layers-1].n_tgt; 1 for a single query). */
+int xpg_masked_forward(const xpg_forward_plan* plan, const uint32_t* bits, int64_t rows,
+                       float* y, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
+
+/* ---------------------------------------------------------------- weighted linear surrogate */
+typedef struct xpg_wlm_params {
+  float lr, l1_lambda, beta1, beta2, eps, weight_decay;
+} xpg_wlm_params;
+
+/* Runs ceil(rows / batch) Adam steps of train_model over consecutive row batches; w, m, v are
+ * updated in place (fp32 [cols]); losses[step] (fp64) and best_epoch (first argmin) written.
+ * `step0` is the number of Adam steps already taken with (m, v) (0 for a fresh optimizer). */
+int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                const float* y, const double* kernel, const xpg_wlm_params* params,
+                int64_t step0, float* w, float* adam_m, float* adam_v, double* losses,
+                int32_t* best_epoch, xpg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XPGNN_H */

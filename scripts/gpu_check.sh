@@ -1,0 +1,24 @@
+#!/bin/bash
+# GPU-box sequence: each step under its own time limit; stop on a fault/abort/timeout
+# (134/139/124/137 or signals), continue past ordinary failures (exit 1).
+mkdir -p gpurun_out
+run() {  # name, seconds, cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  case $rc in 0|1|2|5) return 0 ;; *) echo "STOP after $name (rc=$rc)"; exit $rc ;; esac
+}
+export PYTHONUNBUFFERED=1
+for step in "$@"; do
+  case $step in
+    build) run build 300 python -c "import __graft_entry__ as g; g.build()" ;;
+    tests) run gpu_tests 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    bench) run bench 600 python bench.py ;;
+    prof)  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+  esac
+done

@@ -1,0 +1,308 @@
+"""GPU parity: the HIP engine (through the C-ABI) vs the numpy oracle and the reference's own
+golden vectors.  Tolerances: integer/bit work bit-exact; fp64 KernelSHAP rtol 1e-10 (device
+binomial via lgamma vs scipy); fp32 GNN outputs atol 1e-5; surrogate weights / explanation
+scores atol 1e-4 (BASELINE north_star: 1e-4 fp32)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from golden_utils import CASES, GOLDEN, load_case, oracle_spec, repeat_masks, state_dict
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from bikg_graph_explainability_public_amd import _lib
+    _lib.load()
+
+
+def _eng():
+    from bikg_graph_explainability_public_amd import engine
+    return engine
+
+
+# ------------------------------------------------------------------ masks / perturbation
+@pytest.mark.parametrize("shape", [(1, 1), (3, 7), (5, 31), (7, 32), (9, 33), (64, 1177),
+                                   (513, 20000)])
+def test_pack_unpack_roundtrip(shape):
+    e = _eng()
+    g = torch.Generator().manual_seed(shape[0] * 131 + shape[1])
+    m = torch.rand(shape, generator=g) < 0.37
+    bits = e.pack_masks(m.to(DEV))
+    np.testing.assert_array_equal(bits.cpu().numpy().view(np.uint32), oracle.pack_bits(m.numpy()))
+    back = e.unpack_masks(bits, shape[1]).cpu()
+    assert torch.equal(back, m)
+
+
+def test_edge_keep_known_answer_and_random():
+    """tests/test_data.py:1761-1845 vectors, then random graphs vs the oracle."""
+    e = _eng()
+    m = torch.tensor([[1, 0, 1, 0, 1, 0, 1], [1, 1, 1, 1, 0, 0, 0], [0, 0, 0, 0, 1, 1, 1]],
+                     dtype=torch.bool)
+    ei = torch.tensor([[0, 2, 3, 6, 4, 5], [5, 6, 4, 1, 2, 0]])
+    keep = e.edge_keep(e.pack_masks(m.to(DEV)), 7, ei[0], ei[1]).cpu().numpy()
+    assert np.flatnonzero(keep).tolist() == [1, 4]
+    rng = np.random.default_rng(3)
+    for S, E, B in [(50, 300, 17), (1000, 5000, 40)]:
+        mm = rng.random((B, S)) < 0.5
+        eei = rng.integers(0, S, (2, E))
+        got = e.edge_keep(e.pack_masks(torch.as_tensor(mm).to(DEV)), S,
+                          torch.as_tensor(eei[0]), torch.as_tensor(eei[1])).cpu().numpy()
+        ref, _ = oracle.build_edge_mask(mm, eei)
+        np.testing.assert_array_equal(got, ref)
+
+
+def test_perturb_node_seam():
+    from bikg_graph_explainability_public_amd.data import Data
+    m = torch.tensor([[1, 0, 1, 0, 1, 0, 1], [1, 1, 1, 1, 0, 0, 0], [0, 0, 0, 0, 1, 1, 1]],
+                     dtype=torch.bool, device=DEV)
+    ei = torch.tensor([[0, 2, 3, 6, 4, 5], [5, 6, 4, 1, 2, 0]], device=DEV)
+    pe, et = Data(torch.zeros(7, 4, device=DEV), ei).perturb_node(
+        m, torch.tensor([0, 0, 0, 1, 1, 1], device=DEV))
+    assert pe.cpu().tolist() == [[2, 4], [6, 2]] and et.cpu().tolist() == [0, 1]
+
+
+def test_shapley_sampler_properties():
+    e = _eng()
+    R, S = 4096, 1255
+    a = e.sample_shapley(7, R, S, DEV)
+    b = e.sample_shapley(7, R, S, DEV)
+    assert torch.equal(a, b)
+    m = e.unpack_masks(a, S).float()
+    dens = m.mean().item()
+    assert abs(dens - 0.5) < 0.005
+    assert abs(m.mean(0) - 0.5).max().item() < 0.05
+    tail = a.cpu().numpy().view(np.uint32)[:, -1] >> (S % 32)
+    assert (tail == 0).all()
+    part = e.sample_shapley(7, 100, S, DEV, row_offset=1000)
+    assert torch.equal(part, a[1000:1100])
+    c = e.sample_shapley(8, R, S, DEV)
+    assert not torch.equal(a, c)
+
+
+# ------------------------------------------------------------------ KernelSHAP
+@pytest.mark.parametrize("cols", [9, 200, 1001, 1002, 1500, 3000, 20000])
+def test_shap_kernel_vs_reference(cols):
+    e = _eng()
+    z = np.load(GOLDEN + "/kernels.npz")
+    m = np.unpackbits(z[f"c{cols}_mask_bits"], axis=1, bitorder="little")[:, :cols].astype(bool)
+    got = e.shap_kernel(e.pack_masks(torch.as_tensor(m).to(DEV)), cols).cpu().numpy()
+    ref = z[f"c{cols}_kernel"]
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=0)
+    np.testing.assert_array_equal(got == 0, ref == 0)
+
+
+def test_kernel_class_seam():
+    from bikg_graph_explainability_public_amd.kernels import Kernel
+    m = torch.tensor([[1, 0, 1, 0, 1, 0, 1, 0, 0], [0, 1, 0, 1, 0, 1, 0, 1, 1],
+                      [1, 1, 0, 0, 0, 1, 1, 1, 0], [1, 0, 1, 1, 1, 0, 0, 0, 1]],
+                     dtype=torch.bool, device=DEV)
+    k = Kernel(m).compute().cpu().numpy()
+    np.testing.assert_allclose(k, oracle.shap_kernel(m.cpu().numpy()), rtol=1e-12)
+    assert abs(k.mean() - 1 / 315) < 1e-3  # tests/test_wlm.py:280-291 (~1/305 within 1e-3)
+
+
+# ------------------------------------------------------------------ dense MFMA
+@pytest.mark.parametrize("M,K,N", [(1, 8, 1), (31, 12, 5), (32, 64, 32), (100, 84, 16),
+                                   (257, 128, 256), (1000, 64, 64), (4099, 256, 200)])
+def test_dense_mfma_vs_torch_fp32(M, K, N):
+    e = _eng()
+    g = torch.Generator().manual_seed(M + K + N)
+    A = torch.randn((M, K), generator=g)
+    W = torch.randn((N, K), generator=g) * torch.linspace(0.5, 2.0, K)  # asymmetric
+    b = torch.randn(N, generator=g)
+    for act, fn in [(None, lambda x: x), ("relu", torch.relu), ("sigmoid", torch.sigmoid)]:
+        got = e.dense(A.to(DEV), W.to(DEV), b.to(DEV), act).cpu()
+        ref = fn(A.double() @ W.double().T + b.double()).float()
+        torch.testing.assert_close(got, ref, rtol=0, atol=2e-5 * max(1.0, K ** 0.5))
+
+
+# ------------------------------------------------------------------ masked forward
+def _plan_for(name):
+    from bikg_graph_explainability_public_amd import pipeline
+    from case_builders import build_explainer
+    exp, z, meta = build_explainer(name)
+    ctx = exp.prepare(meta["element"], DEV)
+    plan = pipeline.build_plan(exp.arch, ctx["sub_feat"], ctx["sub_ei"], [ctx["sub_ind"]],
+                               ctx["sub_nt"], ctx["sub_et"], ctx["h_ntypes"], ctx["h_etypes"],
+                               ctx["padded_dims"])
+    return exp, z, meta, ctx, plan
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_masked_forward_vs_reference_outputs(name):
+    e = _eng()
+    exp, z, meta, ctx, plan = _plan_for(name)
+    assert plan is not None, "engine must compile every golden architecture"
+    for i, m in enumerate(repeat_masks(z, meta)):
+        y = plan.forward(e.pack_masks(torch.as_tensor(m).to(DEV)))[:, 0].cpu().numpy()
+        np.testing.assert_allclose(y, z[f"r{i}_output"], rtol=0, atol=1e-5)
+
+
+def test_masked_forward_vs_oracle_fp64():
+    """Same as above against the fp64 oracle on fresh random masks (all golden archs)."""
+    e = _eng()
+    from test_oracle_golden import prepare
+    for name in CASES:
+        zz, meta, spec, sub_x, rel_ei, sub_ind = prepare(name)
+        exp, z, meta, ctx, plan = _plan_for(name)
+        rng = np.random.default_rng(len(name))
+        m = rng.random((97, sub_x.shape[0])) < rng.random((97, 1))
+        ref = oracle.masked_query_outputs(spec, sub_x, rel_ei, m, sub_ind)
+        got = plan.forward(e.pack_masks(torch.as_tensor(m).to(DEV)))[:, 0].cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)
+
+
+def test_generic_path_matches_engine():
+    from bikg_graph_explainability_public_amd import pipeline
+    for name in ["test_run", "hetero_single", "sage_shapley"]:
+        exp, z, meta, ctx, plan = _plan_for(name)
+        ok, err = pipeline.verify_plan(plan, exp.arch, ctx["sub_feat"], ctx["sub_ei"],
+                                       ctx["sub_ind"], ctx["sub_nt"], ctx["sub_et"],
+                                       ctx["h_ntypes"], ctx["h_etypes"], ctx["padded_dims"],
+                                       rows=16)
+        assert ok, (name, err)
+
+
+# ------------------------------------------------------------------ surrogate
+@pytest.mark.parametrize("name", CASES)
+def test_wlm_fit_vs_reference(name):
+    e = _eng()
+    z, meta = load_case(name)
+    for i, m in enumerate(repeat_masks(z, meta)):
+        bits = e.pack_masks(torch.as_tensor(m).to(DEV))
+        w, losses, best, _, _ = e.wlm_fit(bits, m.shape[1], meta[f"r{i}_batch_size"],
+                                          torch.as_tensor(z[f"r{i}_output"]),
+                                          torch.as_tensor(z[f"r{i}_kernel"]),
+                                          torch.as_tensor(z[f"r{i}_w0"]), meta["params"])
+        np.testing.assert_allclose(w.cpu().numpy(), z[f"r{i}_w_final"], rtol=0, atol=1e-4)
+        np.testing.assert_allclose(losses.cpu().numpy(), z[f"r{i}_losses"], rtol=1e-4)
+        assert int(best.item()) == meta[f"r{i}_best_epoch"]
+
+
+def test_wlm_fit_vs_oracle_large():
+    """S=3000 columns (3 columns per thread), B=512, fresh data vs the fp64 oracle."""
+    e = _eng()
+    rng = np.random.default_rng(11)
+    R, S, B = 4096, 3000, 512
+    m = rng.random((R, S)) < 0.5
+    y = rng.random(R).astype(np.float32)
+    k = oracle.shap_kernel(m)
+    w0 = ((rng.random(S) - 0.5) * 0.05).astype(np.float32)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    ref, rl, rb = oracle.train_wlm(m, B, y, k, w0, params)
+    w, losses, best, _, _ = e.wlm_fit(e.pack_masks(torch.as_tensor(m).to(DEV)), S, B,
+                                      torch.as_tensor(y), torch.as_tensor(k),
+                                      torch.as_tensor(w0), params)
+    np.testing.assert_allclose(w.cpu().numpy(), ref, rtol=0, atol=1e-4)
+    np.testing.assert_allclose(losses.cpu().numpy(), rl, rtol=1e-5)
+
+
+# ------------------------------------------------------------------ end to end
+@pytest.mark.parametrize("name", CASES)
+def test_explainer_run_matches_reference_dataframes(name):
+    """Explainer.run on the MI355X vs the reference's own DataFrames (same RNG state)."""
+    from case_builders import build_explainer
+    exp, z, meta = build_explainer(name)
+    torch.set_rng_state(torch.as_tensor(z["rng_state"]))
+    df, pdf = exp.run(meta["element"], meta["times"])
+    assert exp.last_run["engine"]
+    ref = meta["df"]
+    got = df.reindex(ref["index"])
+    np.testing.assert_allclose(got["config_value_mean"].values, ref["config_value_mean"],
+                               atol=1e-4, rtol=0)
+    np.testing.assert_allclose(got["config_value_std"].values, ref["config_value_std"],
+                               atol=1e-4, rtol=0)
+    assert df.columns.tolist() == ["config_value_mean", "config_value_std"]
+    vals = df["config_value_mean"].values
+    assert np.all(vals[:-1] >= vals[1:])
+    if meta["pathway_df"] is None:
+        assert pdf is None
+    else:
+        pref = meta["pathway_df"]
+        assert sorted(pdf.index.tolist()) == sorted(pref["index"])
+        np.testing.assert_allclose(pdf.reindex(pref["index"])["score"].values, pref["score"],
+                                   atol=1e-4, rtol=0)
+
+
+def test_train_model_seam_matches_reference():
+    """wlm.train_model(...) with the reference signature on the golden test_run_t1 batches."""
+    from torch.utils.data import DataLoader
+    from bikg_graph_explainability_public_amd.wlm import LinearRegression, train_model
+    from case_builders import build_explainer
+    exp, z, meta = build_explainer("test_run_t1")
+    ctx = exp.prepare(meta["element"], DEV)
+    m = torch.as_tensor(repeat_masks(z, meta)[0]).to(DEV)
+    lm = LinearRegression(ctx["S"]).to(DEV)
+    with torch.no_grad():
+        lm.layer.weight.copy_(torch.as_tensor(z["r0_w0"]).view(1, -1))
+    w, losses, best = train_model(DataLoader(m, batch_size=meta["r0_batch_size"]), meta["params"],
+                                  ctx["sub_feat"], ctx["sub_ei"], lm, exp.arch, "node",
+                                  ctx["sub_ind"])
+    np.testing.assert_allclose(w[0].detach().cpu().numpy(), z["r0_w_final"], atol=1e-4)
+    assert len(losses) == len(z["r0_losses"]) and best == meta["r0_best_epoch"]
+
+
+def test_device_sampler_run_is_sane():
+    from case_builders import build_explainer
+    exp, z, meta = build_explainer("gcn2_medium", {"mask_sampler": "device"})
+    df, pdf = exp.run(meta["element"], 2)
+    assert pdf is None and not np.isnan(df.values).any() and len(df) == len(meta["df"]["index"])
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_c2_scale_forward_properties():
+    """configs[1] scale (100k nodes / 1M edges, F=64, 2-layer GCN, 12,800 rows): engine vs the
+    oracle on a row subset, plus row-order equivariance and all-on / all-off invariants."""
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.data import Data
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    e = _eng()
+    g = torch.Generator().manual_seed(0)
+    N, E, F = 100_000, 1_000_000, 64
+    feat = torch.randn((N, F), generator=g)
+    ei = torch.randint(0, N, (2, E), generator=g)
+    torch.manual_seed(0)
+    arch = ConvStack("gcn", [64, 64, 64], [64, 1]).eval()
+    sub_feat, sub_ei, _, sub_ind, _, _ = Data(feat.to(DEV), ei.to(DEV)).comp_graph(
+        7, 2, "node", [str(i) for i in range(N)])
+    q = int(sub_ind[0])
+    S = sub_feat.shape[0]
+    plan = pipeline.build_plan(arch.to(DEV), sub_feat, sub_ei, [q])
+    R = 12_800
+    bits = e.sample_shapley(123, R, S, DEV)
+    y = plan.forward(bits)[:, 0]
+    m = e.unpack_masks(bits, S).cpu().numpy()
+    spec = {"convs": [{"kind": "gcn", "rels": [None], "act": "relu",
+                       "params": {None: {"W": arch.conv[2 * i].lin.weight.detach().cpu().numpy(),
+                                         "b": arch.conv[2 * i].bias.detach().cpu().numpy()}}}
+                      for i in range(2)],
+            "fc": [{"W": arch.fc[0].weight.detach().cpu().numpy(),
+                    "b": arch.fc[0].bias.detach().cpu().numpy(), "act": "sigmoid"}]}
+    sel = np.arange(0, R, 200)
+    ref = oracle.masked_query_outputs(spec, sub_feat.cpu().numpy(), {None: sub_ei.cpu().numpy()},
+                                      m[sel], q)
+    np.testing.assert_allclose(y.cpu().numpy()[sel], ref, atol=1e-5, rtol=0)
+    perm = torch.randperm(R, generator=g).to(DEV)
+    y2 = plan.forward(bits[perm].contiguous())[:, 0]
+    torch.testing.assert_close(y2, y[perm], rtol=0, atol=0)
+    on = e.pack_masks(torch.ones((2, S), dtype=torch.bool, device=DEV))
+    off = e.pack_masks(torch.zeros((2, S), dtype=torch.bool, device=DEV))
+    y_on = plan.forward(on)[:, 0].cpu().numpy()
+    y_off = plan.forward(off)[:, 0].cpu().numpy()
+    ref_on = oracle.masked_query_outputs(spec, sub_feat.cpu().numpy(),
+                                         {None: sub_ei.cpu().numpy()}, np.ones((1, S), bool), q)
+    ref_off = oracle.masked_query_outputs(spec, sub_feat.cpu().numpy(),
+                                          {None: sub_ei.cpu().numpy()}, np.zeros((1, S), bool), q)
+    np.testing.assert_allclose(y_on, ref_on[0], atol=1e-5)
+    np.testing.assert_allclose(y_off, ref_off[0], atol=1e-5)
+    k = e.shap_kernel(bits, S)
+    assert torch.isfinite(k).all() and (k >= 0).all()

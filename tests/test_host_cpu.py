@@ -1,0 +1,168 @@
+"""CPU tests of the host side: compat mask sampler vs the reference's masks (golden vectors),
+architecture compilation, receptive-field plan arrays, the native library's exports."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from bikg_graph_explainability_public_amd import _lib
+from bikg_graph_explainability_public_amd.engine import plan_arrays
+from bikg_graph_explainability_public_amd.explainer import set_seed
+from bikg_graph_explainability_public_amd.masks import Mask, dataloader_seed_draw
+from bikg_graph_explainability_public_amd.pathways import Pathways
+from bikg_graph_explainability_public_amd.program import UnsupportedArch, compile_arch
+from bikg_graph_explainability_public_amd.wlm import LinearRegression
+from case_builders import build_arch, build_explainer
+from golden_utils import CASES, load_case, repeat_masks
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_compat_sampler_reproduces_reference_masks(name):
+    """masks.py:262-397 restated with the same torch CPU RNG call order: identical masks, and
+    the surrogate's initial weights (LinearRegression init) follow in the same stream."""
+    exp, z, meta = build_explainer(name)
+    torch.set_rng_state(torch.as_tensor(z["rng_state"]))
+    if meta["times"] == 1:
+        set_seed(meta["params"]["seed"])
+    ctx = exp.prepare(meta["element"], torch.device("cpu"))
+    gold = repeat_masks(z, meta)
+    for i in range(meta["n_repeats"]):
+        mask, rows = Mask(ctx["sub_feat"], ctx["sub_ei"], ctx["sub_pw_inds"], exp.params,
+                          exp.problem).generate()
+        assert mask.shape == gold[i].shape
+        assert np.array_equal(mask.numpy(), gold[i]), f"repeat {i} mask differs"
+        if f"r{i}_pathway_rows" in z.files:
+            assert np.array_equal(rows.numpy(), z[f"r{i}_pathway_rows"])
+        w0 = LinearRegression(ctx["S"]).layer.weight.detach().numpy().reshape(-1)
+        assert np.array_equal(w0, z[f"r{i}_w0"])
+        dataloader_seed_draw()
+        assert mask.shape[0] // meta["params"]["epochs"] == meta[f"r{i}_batch_size"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_prepare_matches_oracle_subgraph(name):
+    exp, z, meta = build_explainer(name)
+    ctx = exp.prepare(meta["element"], torch.device("cpu"))
+    m = repeat_masks(z, meta)[0]
+    assert ctx["S"] == m.shape[1]
+    df_names = set(meta["df"]["index"])
+    assert set(ctx["sub_names"]) == df_names
+
+
+def test_mask_structure_invariant():
+    """tests/test_mask.py:286-393 + tests/test_utils.py:283-356: in every community-mask row
+    at most one community is mixed; the others are all-on or all-off (shared members aside)."""
+    feat = torch.randn(9, 4)
+    ei = torch.tensor([[0, 2, 3, 6, 4, 5, 7, 8], [5, 6, 4, 1, 2, 0, 2, 5]])
+    comms = [[3], [1, 2, 3, 4], [5, 7], [7, 8, 0, 4]]
+    params = {"interpret_samples": 20, "epochs": 50}
+    torch.manual_seed(0)
+    mask, rows = Mask(feat, ei, [list(c) for c in comms], params, "node").generate()
+    assert mask.dtype == torch.bool and mask.shape[1] == 9 and mask.shape[0] >= 1000
+    for r in range(mask.shape[0]):
+        inner = int(rows[r])
+        for i, c in enumerate(comms):
+            if i == inner:
+                continue
+            others = set(e for j, cc in enumerate(comms) if j != i for e in cc)
+            own = [e for e in c if e not in others]
+            if own:
+                vals = mask[r, own]
+                assert bool(vals.all()) or not bool(vals.any())
+
+
+def test_pathway_helpers_known_answers():
+    comm = [[3], [1, 2, 3, 4], [5, 7], [7, 8, 0, 4]]
+    pm = torch.tensor([[0, 0, 0, 0], [0, 0, 0, 1], [0, 1, 0, 0], [0, 0, 1, 0], [0, 0, 1, 0],
+                       [0, 1, 0, 1], [1, 1, 0, 0], [1, 1, 1, 0], [1, 0, 0, 0]], dtype=torch.bool)
+    em, rep = Pathways(comm, None).pathway_mask2node_mask(pm)
+    ref_em, ref_rep = oracle.pathway_mask2node_mask(comm, pm.numpy())
+    assert np.array_equal(em.numpy(), ref_em) and np.array_equal(rep.numpy(), ref_rep)
+    cv = torch.tensor([0.21, 0.23, 0.95, 0.65, 0.98, -0.21, 0.32, 0.94, -0.34])
+    df = Pathways(comm, ["1", "2", "3", "4"]).aggregate(cv, comm)
+    assert df.index.tolist() == ["2", "1", "4", "3"]
+    np.testing.assert_allclose(df["score"].values, [0.7025, 0.65, 0.4475, 0.365], atol=1e-6)
+    hp = {"1": [[0, 1, 2, 3, 4], [5, 6, 7]], "2": [[0, 1, 2], [3, 4, 5]]}
+    res, names, types = Pathways(hp, {"1": ["1", "2"], "2": ["3", "4"]}).hetero2homo("node",
+                                                                                      [0, 8])
+    assert res == [[0, 1, 2, 3, 4], [5, 6, 7], [8, 9, 10], [11, 12, 13]]
+    assert names == ["1", "2", "3", "4"] and types.int().tolist() == [0, 0, 1, 1]
+    dead = torch.zeros((9, 4), dtype=torch.bool)
+    dead[3, 2] = dead[4, 2] = True
+    out = Pathways(comm, None).activate_dead_mask(dead, 2)
+    assert out.shape == dead.shape and not torch.equal(out, dead)
+
+
+@pytest.mark.parametrize("name", ["test_run", "toy", "hetero_single", "sage_shapley",
+                                  "gcn2_medium"])
+def test_compile_arch(name):
+    exp, z, meta = build_explainer(name)
+    rels = meta["arch_spec"].get("hetero_rels")
+    prog = compile_arch(exp.arch, [tuple(r) for r in rels] if rels else None)
+    a = meta["arch_spec"]
+    assert len(prog.convs) == len(a["dims"]) - 1
+    assert len(prog.head) == len(a["fc"]) - 1
+    assert prog.head[-1].act == "sigmoid"
+    assert all(c.act == "relu" for c in prog.convs)
+    if a["kind"] == "sage":
+        assert [t.kind for t in prog.convs[0].terms] == ["mean", "root"]
+    if rels:
+        assert [t.rel for t in prog.convs[0].terms] == [0, 1, 2]
+
+
+def test_compile_rejects_unsupported():
+    class Odd(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.bn = torch.nn.BatchNorm1d(4)
+
+        def forward(self, x, ei):
+            return self.bn(x)
+
+    with pytest.raises(UnsupportedArch):
+        compile_arch(Odd())
+
+
+def test_plan_arrays_receptive_field():
+    rng = np.random.default_rng(0)
+    S, E = 60, 240
+    ei = rng.integers(0, S, size=(2, E))
+    ei[:, :5] = [[3, 4, 5, 6, 7], [3, 4, 5, 6, 7]]  # self-loops
+    q = 3
+    arr = plan_arrays(S, [ei], [q], 2)
+    fr = arr["frontiers"]
+    assert fr[2].tolist() == [q]
+    assert set(fr[1]) == {q} | set(ei[0][ei[1] == q].tolist())
+    assert list(fr[1][:1]) == [q] and list(fr[0][:len(fr[1])]) == list(fr[1])
+    # degree CSR: in-edges (no self loops) of every F0 node
+    for p, v in enumerate(fr[0]):
+        got = sorted(arr["deg_src"][arr["deg_ptr"][p]:arr["deg_ptr"][p + 1]].tolist())
+        exp = sorted(ei[0][(ei[1] == v) & (ei[0] != v)].tolist())
+        assert got == exp
+    lay = arr["layers"][0]
+    for t, v in enumerate(fr[1]):
+        srcs = fr[0][lay["agg_src"][lay["agg_ptr"][t]:lay["agg_ptr"][t + 1]]]
+        assert sorted(srcs.tolist()) == sorted(ei[0][(ei[1] == v) & (ei[0] != v)].tolist())
+        assert lay["self_mult"][t] == int(((ei[0] == v) & (ei[1] == v)).sum())
+
+
+def test_native_library_exports_header_symbols():
+    """libxpgnn.so loads (no GPU needed) and exports every entry point include/xpgnn.h declares."""
+    hdr = open(os.path.join(ROOT, "include", "xpgnn.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(xpg_\w+)\s*\(", hdr, re.M))
+    assert declared == set(_lib.EXPORTED)
+    lib = _lib.load()
+    for name in declared:
+        assert hasattr(lib, name)
+    assert lib.xpg_abi_version() == _lib.ABI_VERSION
+
+
+def test_engine_refuses_cpu_tensors():
+    from bikg_graph_explainability_public_amd import engine
+    with pytest.raises(_lib.NativeLibraryError):
+        engine.pack_masks(torch.zeros((2, 3), dtype=torch.bool))
