@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--epochs", type=int, default=50)
     p.add_argument("--query", type=int, default=7)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-rows", type=int, default=2560)
+    p.add_argument("--cpu-rows", type=int, default=12800)
     return p.parse_args()
 
 

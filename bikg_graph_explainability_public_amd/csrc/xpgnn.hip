@@ -185,6 +185,18 @@ __device__ double block_sum_d(double v, double* red) {
   return s;
 }
 
+// Kernel.compute exact branch (M = S-1 <= 1000, kernels.py:83-113): thread per row.
+__global__ void k_shap_exact(const int32_t* __restrict__ cnt, int64_t rows, int64_t cols,
+                             double* __restrict__ out) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const int64_t Mi = cols - 1;
+  const double M = static_cast<double>(Mi);
+  const int64_t k = cnt[r];
+  const double choose = binom_d(M + 1.0, static_cast<double>(k));
+  out[r] = clean_inf(M / (choose * static_cast<double>(Mi + 1 - k) * static_cast<double>(k)));
+}
+
 // Kernel.compute (kernels.py:115-174).  Exact branch is row-parallel; the approximate branch
 // runs the reference's ref back-off loop (sum == 0 -> ref = int(0.9 ref)) in this one block.
 __global__ __launch_bounds__(1024) void k_shap(const int32_t* __restrict__ cnt, int64_t rows,
@@ -434,26 +446,103 @@ __global__ void k_take_col(const float* __restrict__ C, int64_t M, int64_t ldc, 
 }
 
 // ------------------------------------------------------------------------------------ surrogate
-// train_model (wlm.py:132-278) in one persistent 1024-thread workgroup: every Adam step's batch
-// of mask words is staged transposed in LDS ([word][row], odd row pitch), predictions are
-// bit-scans over w (LDS, 33-float pitch per 32 columns), the loss/gradient use the reference's
-// [B] - [B,1] broadcast in closed form (quirk Q1), parameters stay in registers (CPT per thread).
-template <int CPT>
-__global__ __launch_bounds__(1024) void k_wlm(const uint32_t* __restrict__ bits, int64_t rows,
-                                              int cols, int words, int batch, int pitch,
-                                              const float* __restrict__ y,
-                                              const double* __restrict__ kern, xpg_wlm_params P,
-                                              int64_t step0, float* __restrict__ wg,
-                                              float* __restrict__ mg, float* __restrict__ vg,
-                                              double* __restrict__ losses,
-                                              int32_t* __restrict__ best_epoch) {
+// train_model (wlm.py:132-278) in three stages:
+//  1. k_wlm_stats  (grid, block per Adam step): per-step constants that do not depend on w —
+//     mean(y), sum(k), sum (y - mean)^2 — and the Adam bias corrections (step size, sqrt(bc2)).
+//  2. k_wlm_colbits (grid, wave per (step, word, 64-row chunk)): transposes each step's mask
+//     batch into per-column row bit vectors with 32 wave ballots, for the gradient M_b^T g.
+//  3. k_wlm_fit (ONE persistent 1024-thread workgroup: the Adam steps are strictly sequential):
+//     per step, 4-bit lookup tables of w (T[col/4][16]) turn p = M_b w into one LDS lookup per
+//     nibble of a mask row; tables of g (G[row/4][16]) turn M_b^T g into one lookup per nibble of
+//     a column's row vector; parameters and Adam moments stay in registers (CPT per thread).
+//     The loss (closed form of the reference's [B] - [B,1] broadcast, quirk Q1) is computed
+//     afterwards by k_wlm_loss from the recorded predictions and pre-step weights.
+struct WlmStep {
+  double ybar, ksum, vy;
+  float step_size, bc2_sqrt;
+};
+
+__global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
+                                                   const double* __restrict__ kern, int64_t rows,
+                                                   int batch, xpg_wlm_params P, int64_t step0,
+                                                   WlmStep* __restrict__ st) {
+  __shared__ double red[16];
+  const int64_t t = blockIdx.x;
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  double sy = 0.0, sk = 0.0;
+  for (int j = threadIdx.x; j < B; j += blockDim.x) {
+    sy += static_cast<double>(y[r0 + j]);
+    sk += kern[r0 + j];
+  }
+  const double Sy = block_sum_d(sy, red);
+  const double Sk = block_sum_d(sk, red);
+  const double ybar = Sy / B;
+  double vy = 0.0;
+  for (int j = threadIdx.x; j < B; j += blockDim.x) {
+    const double d = static_cast<double>(y[r0 + j]) - ybar;
+    vy += d * d;
+  }
+  const double Vy = block_sum_d(vy, red);
+  if (threadIdx.x == 0) {
+    const double step = static_cast<double>(step0 + t + 1);
+    const double bc1 = 1.0 - pow(static_cast<double>(P.beta1), step);
+    const double bc2 = 1.0 - pow(static_cast<double>(P.beta2), step);
+    WlmStep w;
+    w.ybar = ybar;
+    w.ksum = Sk;
+    w.vy = Vy;
+    w.step_size = static_cast<float>(static_cast<double>(P.lr) / bc1);
+    w.bc2_sqrt = static_cast<float>(sqrt(bc2));
+    st[t] = w;
+  }
+}
+
+// colbits[(t * cols + c) * bw + jw] bit b = mask bit (row t*batch + 32*jw + b, column c)
+__global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict__ bits, int64_t rows,
+                                                     int cols, int words, int batch, int bw,
+                                                     int64_t steps, uint32_t* __restrict__ colbits) {
+  const int lane = threadIdx.x & 63;
+  const int chunks = (batch + 63) / 64;
+  const int64_t wave = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wave >= steps * words * chunks) return;  // wave-uniform exit
+  const int64_t t = wave / ((int64_t)words * chunks);
+  const int rem = static_cast<int>(wave - t * words * chunks);
+  const int wd = rem / chunks, ch = rem - wd * chunks;
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const int j = ch * 64 + lane;
+  const uint32_t word = j < B ? bits[(r0 + j) * words + wd] : 0u;
+#pragma unroll 4
+  for (int c = 0; c < 32; ++c) {
+    const unsigned long long m = __ballot((word >> c) & 1u);
+    const int col = wd * 32 + c;
+    if (lane == c && col < cols) {
+      uint32_t* dst = colbits + ((int64_t)t * cols + col) * bw + 2 * ch;
+      dst[0] = static_cast<uint32_t>(m);
+      if (2 * ch + 1 < bw) dst[1] = static_cast<uint32_t>(m >> 32);
+    }
+  }
+}
+
+constexpr int kTabPitch = 17;  // 16 entries + 1 pad (bank spread across tables)
+
+template <int CPT, bool T_IN_LDS>
+__global__ __launch_bounds__(1024) void k_wlm_fit(
+    const uint32_t* __restrict__ bits, const uint32_t* __restrict__ colbits, int64_t rows,
+    int cols, int words, int batch, int bw, const double* __restrict__ kern,
+    const WlmStep* __restrict__ stp, xpg_wlm_params P, float* __restrict__ wg,
+    float* __restrict__ mg, float* __restrict__ vg, float* __restrict__ p_hist,
+    float* __restrict__ w_hist, float* __restrict__ t_glob) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* red = reinterpret_cast<double*>(smem);                 // [32]
-  float* w_s = reinterpret_cast<float*>(smem + 256);              // [words * 33]
-  float* p_s = w_s + ((words * 33 + 3) & ~3);                     // [pitch]
-  float* g_s = p_s + pitch;                                       // [pitch]
-  uint32_t* wt = reinterpret_cast<uint32_t*>(g_s + pitch);        // [words][pitch]
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = blockDim.x >> 6;
+  const int tid = threadIdx.x;
+  const int ntab = words * 8;      // one table per nibble of every word (tail nibbles read 0s)
+  const int cols_pad = words * 32;
+  const int ngrp = (batch + 3) / 4;
+  float* w_s = reinterpret_cast<float*>(smem);               // [cols_pad]
+  float* g_s = w_s + cols_pad;                                // [ngrp * 4]
+  float* G = g_s + ngrp * 4;                                  // [ngrp * 17]
+  float* T = T_IN_LDS ? (G + ngrp * kTabPitch) : t_glob;      // [words * 8 * 17]
 
   float w[CPT], m[CPT], v[CPT];
 #pragma unroll
@@ -463,103 +552,100 @@ __global__ __launch_bounds__(1024) void k_wlm(const uint32_t* __restrict__ bits,
     m[c] = i < cols ? mg[i] : 0.f;
     v[c] = i < cols ? vg[i] : 0.f;
   }
+  for (int i = tid; i < cols_pad; i += 1024) w_s[i] = i < cols ? wg[i] : 0.f;
+  __syncthreads();
+
+  // threads per mask row in the prediction: power of two, rows x TPR ~ 1024
+  int tpr = 64;
+  while (tpr > 1 && (1024 / tpr) < batch) tpr >>= 1;
+  const int rows_per_pass = 1024 / tpr;
+  const int sub = tid & (tpr - 1);
+  const int passes = (batch + rows_per_pass - 1) / rows_per_pass;
+  const float l1s = P.l1_lambda / static_cast<float>(cols);
   const int64_t nsteps = (rows + batch - 1) / batch;
-  double best = INFINITY;
-  int best_e = 0;
-  const float inv_cols = 1.f / static_cast<float>(cols);
+
   for (int64_t t = 0; t < nsteps; ++t) {
     const int64_t r0 = t * batch;
     const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
-    // stage batch words transposed (zero the row padding) and the current w
-    for (int idx = tid; idx < words * pitch; idx += blockDim.x) {
-      const int wd = idx / pitch, j = idx - wd * pitch;
-      wt[idx] = j < B ? bits[(r0 + j) * words + wd] : 0u;
+    const WlmStep sc = stp[t];
+    // A: nibble tables of w; record the pre-step weights (loss regulariser term)
+    for (int e = tid; e < ntab * 16; e += 1024) {
+      const int tb = e >> 4, vv = e & 15;
+      const float* wb = w_s + tb * 4;
+      float s = 0.f;
+      s += (vv & 1) ? wb[0] : 0.f;
+      s += (vv & 2) ? wb[1] : 0.f;
+      s += (vv & 4) ? wb[2] : 0.f;
+      s += (vv & 8) ? wb[3] : 0.f;
+      T[tb * kTabPitch + vv] = s;
     }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int i = tid + c * 1024;
-      if (i < cols) w_s[(i >> 5) * 33 + (i & 31)] = w[c];
+      if (i < cols) w_hist[t * cols + i] = w[c];
     }
     __syncthreads();
-    // predictions p_j = sum_i M[j,i] w_i
-    for (int j = wv; j < B; j += nwv) {
+    if (!T_IN_LDS) __threadfence_block();
+    // B: predictions p_j = M_b[j] . w, then g_j = 2 k_j (p_j - ybar) / (B sum k)
+    for (int ps = 0; ps < passes; ++ps) {
+      const int j = ps * rows_per_pass + tid / tpr;
       float s = 0.f;
-      for (int wd = lane; wd < words; wd += 64) {
-        uint32_t word = wt[wd * pitch + j];
-        const float* wb = w_s + wd * 33;
-        while (word) {
-          const int c = __ffs(word) - 1;
-          s += wb[c];
-          word &= word - 1u;
+      if (j < B) {
+        const uint32_t* row = bits + (r0 + j) * words;
+        for (int wd = sub; wd < words; wd += tpr) {
+          const uint32_t word = row[wd];
+          const float* tw = T + (wd * 8) * kTabPitch;
+#pragma unroll
+          for (int nb = 0; nb < 8; ++nb) s += tw[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
         }
       }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      if (lane == 0) p_s[j] = s;
+      for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+      if (sub == 0 && j < ngrp * 4) {
+        float g = 0.f;
+        if (j < B) {
+          p_hist[r0 + j] = s;
+          const double kj = kern[r0 + j];
+          g = static_cast<float>(2.0 * kj * (static_cast<double>(s) - sc.ybar) /
+                                 (static_cast<double>(B) * sc.ksum));
+        }
+        g_s[j] = g;
+      }
     }
-    // per-step constants (independent of w): sum y, sum k
-    double sy = 0.0, sk = 0.0, sa = 0.0;
-    for (int j = tid; j < B; j += blockDim.x) {
-      sy += static_cast<double>(y[r0 + j]);
-      sk += kern[r0 + j];
+    __syncthreads();
+    // C: nibble tables of g over groups of 4 rows
+    for (int e = tid; e < ngrp * 16; e += 1024) {
+      const int gr = e >> 4, vv = e & 15;
+      const float* gb = g_s + gr * 4;
+      float s = 0.f;
+      s += (vv & 1) ? gb[0] : 0.f;
+      s += (vv & 2) ? gb[1] : 0.f;
+      s += (vv & 4) ? gb[2] : 0.f;
+      s += (vv & 8) ? gb[3] : 0.f;
+      G[gr * kTabPitch + vv] = s;
     }
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) sa += fabs(static_cast<double>(w[c]));
-    const double Sy = block_sum_d(sy, red);
-    const double Sk = block_sum_d(sk, red);
-    const double Sa = block_sum_d(sa, red);
-    const double ybar = Sy / B;
-    double vy = 0.0, tk = 0.0;
-    for (int j = tid; j < B; j += blockDim.x) {
-      const double dy = static_cast<double>(y[r0 + j]) - ybar;
-      const double dp = static_cast<double>(p_s[j]) - ybar;
-      const double kj = kern[r0 + j];
-      vy += dy * dy;
-      tk += kj * dp * dp;
-      g_s[j] = static_cast<float>(2.0 * kj * dp / (static_cast<double>(B) * Sk));
-    }
-    for (int j = B + tid; j < pitch; j += blockDim.x) g_s[j] = 0.f;
-    const double Vy = block_sum_d(vy, red);
-    const double Tk = block_sum_d(tk, red);
-    // loss = mean_ij k_j (p_j - y_i)^2 / sum k + l1 * mean|w|   (wlm.py:240-243, 517-518)
-    const float reg = P.l1_lambda * static_cast<float>(Sa / cols);
-    const double loss = Tk / (static_cast<double>(B) * Sk) + Vy / (static_cast<double>(B) * B) +
-                        static_cast<double>(reg);
-    // gradient + Adam (torch single-tensor Adam with L2 weight decay)
-    const int64_t step = step0 + t + 1;
-    const double bc1 = 1.0 - pow(static_cast<double>(P.beta1), static_cast<double>(step));
-    const double bc2 = 1.0 - pow(static_cast<double>(P.beta2), static_cast<double>(step));
-    const float step_size = static_cast<float>(static_cast<double>(P.lr) / bc1);
-    const float bc2_sqrt = static_cast<float>(sqrt(bc2));
+    __syncthreads();
+    // D: gradient M_b^T g + L1 subgradient + L2 decay, Adam (torch single-tensor order)
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int i = tid + c * 1024;
       if (i < cols) {
-        const uint32_t* col = wt + (i >> 5) * pitch;
-        const int bit = i & 31;
+        const uint32_t* cb = colbits + (t * cols + i) * bw;
         float s = 0.f;
-        for (int j = 0; j < B; j += 4) {
-          const uint4 q = *reinterpret_cast<const uint4*>(col + j);
-          const float4 gq = *reinterpret_cast<const float4*>(g_s + j);
-          s += ((q.x >> bit) & 1u) ? gq.x : 0.f;
-          s += ((q.y >> bit) & 1u) ? gq.y : 0.f;
-          s += ((q.z >> bit) & 1u) ? gq.z : 0.f;
-          s += ((q.w >> bit) & 1u) ? gq.w : 0.f;
+        for (int jw = 0; jw < bw; ++jw) {
+          const uint32_t word = cb[jw];
+          const int g0 = jw * 8;
+#pragma unroll
+          for (int nb = 0; nb < 8; ++nb)
+            if (g0 + nb < ngrp) s += G[(g0 + nb) * kTabPitch + ((word >> (4 * nb)) & 15u)];
         }
         const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
-        float g = s + P.l1_lambda * inv_cols * sg;
+        float g = fmaf(l1s, sg, s);
         g = fmaf(P.weight_decay, w[c], g);
         m[c] = fmaf(1.f - P.beta1, g - m[c], m[c]);
         v[c] = fmaf(1.f - P.beta2, g * g, v[c] * P.beta2);
-        const float denom = sqrtf(v[c]) / bc2_sqrt + P.eps;
-        w[c] = w[c] - step_size * (m[c] / denom);
-      }
-    }
-    if (tid == 0) {
-      losses[t] = loss;
-      if (loss < best) {
-        best = loss;
-        best_e = static_cast<int>(t);
+        const float denom = sqrtf(v[c]) / sc.bc2_sqrt + P.eps;
+        w[c] = w[c] - sc.step_size * (m[c] / denom);
+        w_s[i] = w[c];
       }
     }
     __syncthreads();
@@ -573,7 +659,45 @@ __global__ __launch_bounds__(1024) void k_wlm(const uint32_t* __restrict__ bits,
       vg[i] = v[c];
     }
   }
-  if (tid == 0) best_epoch[0] = best_e;
+}
+
+// loss_t = sum_j k_j (p_j - ybar)^2 / (B sum k) + sum_i (y_i - ybar)^2 / B^2 + l1 * mean|w_t|
+__global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hist,
+                                                  const float* __restrict__ w_hist,
+                                                  const double* __restrict__ kern,
+                                                  const WlmStep* __restrict__ stp, int64_t rows,
+                                                  int cols, int batch, float l1,
+                                                  double* __restrict__ losses) {
+  __shared__ double red[16];
+  const int64_t t = blockIdx.x;
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const WlmStep sc = stp[t];
+  double tk = 0.0, sa = 0.0;
+  for (int j = threadIdx.x; j < B; j += blockDim.x) {
+    const double d = static_cast<double>(p_hist[r0 + j]) - sc.ybar;
+    tk += kern[r0 + j] * d * d;
+  }
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) sa += fabs(static_cast<double>(w_hist[t * cols + i]));
+  const double Tk = block_sum_d(tk, red);
+  const double Sa = block_sum_d(sa, red);
+  if (threadIdx.x == 0) {
+    const float reg = l1 * static_cast<float>(Sa / cols);
+    losses[t] = Tk / (static_cast<double>(B) * sc.ksum) + sc.vy / (static_cast<double>(B) * B) +
+                static_cast<double>(reg);
+  }
+}
+
+__global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double best = INFINITY;
+  int32_t bi = 0;
+  for (int64_t i = 0; i < n; ++i)
+    if (v[i] < best) {
+      best = v[i];
+      bi = static_cast<int32_t>(i);
+    }
+  *out = bi;
 }
 
 // ------------------------------------------------------------------------------------ helpers
@@ -715,7 +839,11 @@ int xpg_popcount_rows(const uint32_t* bits, int64_t rows, int64_t cols, int32_t*
 int xpg_shap_kernel(const int32_t* counts, int64_t rows, int64_t cols, double* kernel_out, xpg_stream_t stream) {
   XPG_REQ(rows >= 0 && cols > 1, "shap_kernel: need cols > 1");
   if (rows == 0) return XPG_OK;
-  hipLaunchKernelGGL(k_shap, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
+  if (cols - 1 <= 1000)
+    hipLaunchKernelGGL(k_shap_exact, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream), counts,
+                       rows, cols, kernel_out);
+  else
+    hipLaunchKernelGGL(k_shap, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
   XPG_LAUNCHED();
   return XPG_OK;
 }
@@ -820,31 +948,96 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   return XPG_OK;
 }
 
+struct WlmWs {
+  size_t steps_off, colbits_off, phist_off, whist_off, tglob_off, total;
+  int bw;
+  bool t_in_lds;
+  size_t lds;
+};
+
+static int wlm_layout(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
+  XPG_REQ(rows > 0 && cols > 0 && batch > 0, "wlm_fit: bad arguments");
+  XPG_REQ(cols <= 16 * 1024, "wlm_fit: more than 16384 columns is not supported by the single-workgroup fit");
+  XPG_REQ(batch <= 1 << 20, "wlm_fit: batch too large");
+  const int64_t steps = cdiv(rows, batch);
+  const int words = words_of(cols);
+  L->bw = static_cast<int>(cdiv(batch, 32));
+  const int64_t ngrp = cdiv(batch, 4);
+  const size_t base_lds = sizeof(float) * (size_t)((int64_t)words * 32 + ngrp * 4 + ngrp * kTabPitch);
+  const size_t t_bytes = sizeof(float) * (size_t)words * 8 * kTabPitch;
+  XPG_REQ(base_lds <= 150 * 1024, "wlm_fit: batch x columns too large for the single-workgroup fit (LDS)");
+  L->t_in_lds = base_lds + t_bytes <= 150 * 1024;
+  L->lds = base_lds + (L->t_in_lds ? t_bytes : 0);
+  size_t off = 0;
+  L->steps_off = off;
+  off += align_up(sizeof(WlmStep) * (size_t)steps);
+  L->colbits_off = off;
+  off += align_up(sizeof(uint32_t) * (size_t)steps * cols * L->bw);
+  L->phist_off = off;
+  off += align_up(sizeof(float) * (size_t)rows);
+  L->whist_off = off;
+  off += align_up(sizeof(float) * (size_t)steps * cols);
+  L->tglob_off = off;
+  off += align_up(L->t_in_lds ? 0 : t_bytes);
+  L->total = off;
+  return XPG_OK;
+}
+
+int xpg_wlm_workspace(int64_t rows, int64_t cols, int64_t batch, size_t* bytes) {
+  WlmWs L;
+  int rc = wlm_layout(rows, cols, batch, &L);
+  if (rc) return rc;
+  *bytes = L.total;
+  return XPG_OK;
+}
+
 int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch, const float* y,
                 const double* kernel, const xpg_wlm_params* params, int64_t step0, float* w,
-                float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, xpg_stream_t stream) {
-  XPG_REQ(rows > 0 && cols > 0 && batch > 0 && params, "wlm_fit: bad arguments");
-  const int words = words_of(cols);
-  const int64_t pitch = ((batch + 3) & ~int64_t(3)) + 4 * ((((batch + 3) / 4) & 1) == 0);  // odd # of 16B slots
-  const size_t lds = 256 + sizeof(float) * (((size_t)words * 33 + 3) & ~size_t(3)) +
-                     sizeof(float) * 2 * pitch + sizeof(uint32_t) * (size_t)words * pitch;
-  XPG_REQ(lds <= 160 * 1024, "wlm_fit: batch x columns too large for the single-workgroup fit (LDS)");
-  XPG_REQ(cols <= 16 * 1024, "wlm_fit: more than 16384 columns not supported by the single-workgroup fit");
-  const int cpt = static_cast<int>(cdiv(cols, 1024));
+                float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, void* workspace,
+                size_t workspace_bytes, xpg_stream_t stream) {
+  XPG_REQ(params != nullptr, "wlm_fit: params required");
+  WlmWs L;
+  int rc = wlm_layout(rows, cols, batch, &L);
+  if (rc) return rc;
+  XPG_REQ(workspace_bytes >= L.total, "wlm_fit: workspace too small");
   hipStream_t st = S(stream);
-  const int ic = static_cast<int>(cols), ib = static_cast<int>(batch), ip = static_cast<int>(pitch);
-#define XPG_WLM(C)                                                                                          \
-  if (cpt <= C) {                                                                                           \
-    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm<C>),                                   \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));        \
-    hipLaunchKernelGGL(k_wlm<C>, dim3(1), dim3(1024), lds, st, bits, rows, ic, words, ib, ip, y, kernel,    \
-                       *params, step0, w, adam_m, adam_v, losses, best_epoch);                              \
-    XPG_LAUNCHED();                                                                                         \
-    return XPG_OK;                                                                                          \
+  char* ws = static_cast<char*>(workspace);
+  WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
+  uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
+  float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
+  float* w_hist = reinterpret_cast<float*>(ws + L.whist_off);
+  float* t_glob = reinterpret_cast<float*>(ws + L.tglob_off);
+  const int64_t steps = cdiv(rows, batch);
+  const int words = words_of(cols);
+  const int ic = static_cast<int>(cols), ib = static_cast<int>(batch);
+  hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps)), dim3(256), 0, st, y, kernel, rows, ib,
+                     *params, step0, stp);
+  XPG_LAUNCHED();
+  const int64_t waves = steps * words * cdiv(batch, 64);
+  hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(waves, 4))), dim3(256), 0, st, bits, rows, ic,
+                     words, ib, L.bw, steps, colbits);
+  XPG_LAUNCHED();
+  const int cpt = static_cast<int>(cdiv(cols, 1024));
+#define XPG_WLM(C, TL)                                                                                     \
+  if (cpt <= C && L.t_in_lds == TL) {                                                                      \
+    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit<C, TL>),                          \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds)));     \
+    hipLaunchKernelGGL((k_wlm_fit<C, TL>), dim3(1), dim3(1024), L.lds, st, bits, colbits, rows, ic, words, \
+                       ib, L.bw, kernel, stp, *params, w, adam_m, adam_v, p_hist, w_hist, t_glob);         \
+    XPG_LAUNCHED();                                                                                        \
+    goto fitted;                                                                                           \
   }
-  XPG_WLM(1) XPG_WLM(2) XPG_WLM(4) XPG_WLM(8) XPG_WLM(16)
+  XPG_WLM(1, true) XPG_WLM(2, true) XPG_WLM(4, true) XPG_WLM(8, true) XPG_WLM(16, true)
+  XPG_WLM(1, false) XPG_WLM(2, false) XPG_WLM(4, false) XPG_WLM(8, false) XPG_WLM(16, false)
 #undef XPG_WLM
   return fail(XPG_EINVAL, "wlm_fit: unsupported column count");
+fitted:
+  hipLaunchKernelGGL(k_wlm_loss, dim3(static_cast<unsigned>(steps)), dim3(256), 0, st, p_hist, w_hist, kernel,
+                     stp, rows, ic, ib, params->l1_lambda, losses);
+  XPG_LAUNCHED();
+  hipLaunchKernelGGL(k_argmin_first, dim3(1), dim3(64), 0, st, losses, steps, best_epoch);
+  XPG_LAUNCHED();
+  return XPG_OK;
 }
 
 }  // extern "C"

@@ -299,6 +299,19 @@ class ForwardPlan:
 
 
 # ----------------------------------------------------------------------------- surrogate
+_WS = {}
+
+
+def _workspace(dev, nbytes):
+    """Reusable per-device scratch (stream-ordered reuse: every user is on the current stream)."""
+    key = (dev.type, dev.index)
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        _WS[key] = t
+    return t
+
+
 def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0):
     """train_model (wlm.py:132-278) epoch loop on device.  Returns (w, losses, best_epoch,
     adam_m, adam_v)."""
@@ -317,6 +330,10 @@ def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0)
                   beta2=0.999, eps=1e-8, weight_decay=1e-2)
     yy = y.to(device=dev, dtype=torch.float32).contiguous()
     kk = kernel.to(device=dev, dtype=torch.float64).contiguous()
+    n = ctypes.c_size_t(0)
+    _lib.check(_lib.load().xpg_wlm_workspace(rows, cols, batch, ctypes.byref(n)))
+    ws = _workspace(dev, n.value)
     call("xpg_wlm_fit", ptr(bits), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
-         int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), _lib.stream_of(dev))
+         int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(ws), ws.numel(),
+         _lib.stream_of(dev))
     return w, losses, best, m, v

@@ -182,6 +182,7 @@ class Explainer:
         device = torch.device("cuda", torch.cuda.current_device())
         if times == 1:
             set_seed(self.params["seed"])
+        self.arch = self.arch.to(device).eval()
         c = self.prepare(element, device)
         sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 1
+#define XPG_ABI_VERSION 2
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -145,13 +145,16 @@ typedef struct xpg_wlm_params {
   float lr, l1_lambda, beta1, beta2, eps, weight_decay;
 } xpg_wlm_params;
 
+/* Workspace needed by xpg_wlm_fit. */
+int xpg_wlm_workspace(int64_t rows, int64_t cols, int64_t batch, size_t* bytes);
 /* Runs ceil(rows / batch) Adam steps of train_model over consecutive row batches; w, m, v are
  * updated in place (fp32 [cols]); losses[step] (fp64) and best_epoch (first argmin) written.
  * `step0` is the number of Adam steps already taken with (m, v) (0 for a fresh optimizer). */
 int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                 const float* y, const double* kernel, const xpg_wlm_params* params,
                 int64_t step0, float* w, float* adam_m, float* adam_v, double* losses,
-                int32_t* best_epoch, xpg_stream_t stream);
+                int32_t* best_epoch, void* workspace, size_t workspace_bytes,
+                xpg_stream_t stream);
 
 #ifdef __cplusplus
 }

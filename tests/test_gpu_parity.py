@@ -130,6 +130,7 @@ def _plan_for(name):
     from bikg_graph_explainability_public_amd import pipeline
     from case_builders import build_explainer
     exp, z, meta = build_explainer(name)
+    exp.arch = exp.arch.to(DEV)
     ctx = exp.prepare(meta["element"], DEV)
     plan = pipeline.build_plan(exp.arch, ctx["sub_feat"], ctx["sub_ei"], [ctx["sub_ind"]],
                                ctx["sub_nt"], ctx["sub_et"], ctx["h_ntypes"], ctx["h_etypes"],
@@ -239,6 +240,7 @@ def test_train_model_seam_matches_reference():
     from bikg_graph_explainability_public_amd.wlm import LinearRegression, train_model
     from case_builders import build_explainer
     exp, z, meta = build_explainer("test_run_t1")
+    exp.arch = exp.arch.to(DEV)
     ctx = exp.prepare(meta["element"], DEV)
     m = torch.as_tensor(repeat_masks(z, meta)[0]).to(DEV)
     lm = LinearRegression(ctx["S"]).to(DEV)
