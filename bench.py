@@ -146,7 +146,7 @@ def main():
     S = plan.cols
     R = args.interpret_samples * args.epochs
     batch = R // args.epochs
-    w0 = torch.zeros(S)
+    w0 = torch.zeros(S, device=dev)
     params = {"lr": 0.01, "l1_lambda": 1e-4}
     stream = torch.cuda.current_stream()
     ev = {k: [] for k in ("sample", "forward", "shap", "wlm")}

@@ -197,37 +197,41 @@ __global__ void k_shap_exact(const int32_t* __restrict__ cnt, int64_t rows, int6
   out[r] = clean_inf(M / (choose * static_cast<double>(Mi + 1 - k) * static_cast<double>(k)));
 }
 
-// Kernel.compute (kernels.py:115-174).  Exact branch is row-parallel; the approximate branch
-// runs the reference's ref back-off loop (sum == 0 -> ref = int(0.9 ref)) in this one block.
-__global__ __launch_bounds__(1024) void k_shap(const int32_t* __restrict__ cnt, int64_t rows,
-                                               int64_t cols, double* __restrict__ out) {
+// Approximate branch (M > 1000, kernels.py:23-80): value of one row at reference size `ref`.
+__device__ __forceinline__ double shap_approx_row(int64_t k, int64_t Mi, int ref) {
+  const double M = static_cast<double>(Mi);
+  int64_t idx = static_cast<int64_t>(static_cast<float>(k * 1000) / static_cast<float>(Mi));
+  idx = idx < 0 ? 0 : (idx > ref - 1 ? ref - 1 : idx);
+  const double choose = (binom_d(static_cast<double>(ref), static_cast<double>(idx)) + 1e-10) * M / 1000.0;
+  return M / (choose * static_cast<double>(k) * static_cast<double>(Mi - k));
+}
+
+// pass 1 (grid): every row at ref = 1000 (raw values, +-inf kept for the sum test)
+__global__ void k_shap_approx_rows(const int32_t* __restrict__ cnt, int64_t rows, int64_t cols,
+                                   double* __restrict__ out) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r < rows) out[r] = shap_approx_row(cnt[r], cols - 1, 1000);
+}
+
+// pass 2 (one block): the reference's loop `while sum(kernel) == 0 and ref > 0` (kernels.py:
+// 148-162) — normally one sum test; the ref = int(0.9 ref) back-off recomputes rows in-block —
+// then +-inf / NaN -> 0 (kernels.py:172).
+__global__ __launch_bounds__(1024) void k_shap_approx_finish(const int32_t* __restrict__ cnt,
+                                                             int64_t rows, int64_t cols,
+                                                             double* __restrict__ out) {
   __shared__ double red[16];
   const int64_t Mi = cols - 1;
-  const double M = static_cast<double>(Mi);
-  if (Mi <= 1000) {
-    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) {
-      const int64_t k = cnt[r];
-      const double choose = binom_d(M + 1.0, static_cast<double>(k));
-      out[r] = clean_inf(M / (choose * static_cast<double>(Mi + 1 - k) * static_cast<double>(k)));
-    }
-    return;
-  }
   int ref = 1000;
   for (;;) {
     double part = 0.0;
-    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) {
-      const int64_t k = cnt[r];
-      int64_t idx = static_cast<int64_t>(static_cast<float>(k * 1000) / static_cast<float>(Mi));
-      idx = idx < 0 ? 0 : (idx > ref - 1 ? ref - 1 : idx);
-      const double choose = (binom_d(static_cast<double>(ref), static_cast<double>(idx)) + 1e-10) * M / 1000.0;
-      const double v = M / (choose * static_cast<double>(k) * static_cast<double>(Mi - k));
-      out[r] = v;
-      part += v;
-    }
+    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) part += out[r];
     const double sum = block_sum_d(part, red);
     if (sum > 0.0) break;
     ref = static_cast<int>(0.9 * static_cast<double>(ref));
     if (!(sum == 0.0 && ref > 0)) break;
+    __syncthreads();
+    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) out[r] = shap_approx_row(cnt[r], Mi, ref);
+    __syncthreads();
   }
   __syncthreads();
   for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) out[r] = clean_inf(out[r]);
@@ -526,6 +530,35 @@ __global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict_
 }
 
 constexpr int kTabPitch = 17;  // 16 entries + 1 pad (bank spread across tables)
+constexpr int kNW = 12;        // prefetched mask words per thread (prediction)
+constexpr int kBW = 8;         // prefetched column words per owned column (gradient, B <= 256)
+
+// In-wave rebuild of the w nibble tables: the 4 columns of table g are owned by 4 adjacent
+// lanes (column i = tid + 1024 c), so each lane shuffles its group's 4 weights and writes 4 of
+// the 16 entries.  Columns >= cols hold w = 0, so tail tables are zero.
+template <int CPT>
+__device__ __forceinline__ void wlm_build_T(const float (&w)[CPT], float* T, int ntab) {
+  const int lane = threadIdx.x & 63, q = lane & 3, base = lane & ~3;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    float wb[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) wb[b] = __shfl(w[c], base + b, 64);
+    const int grp = (static_cast<int>(threadIdx.x) >> 2) + 256 * c;
+    if (grp < ntab) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int vv = q * 4 + e;
+        float s = 0.f;
+        s += (vv & 1) ? wb[0] : 0.f;
+        s += (vv & 2) ? wb[1] : 0.f;
+        s += (vv & 4) ? wb[2] : 0.f;
+        s += (vv & 8) ? wb[3] : 0.f;
+        T[grp * kTabPitch + vv] = s;
+      }
+    }
+  }
+}
 
 template <int CPT, bool T_IN_LDS>
 __global__ __launch_bounds__(1024) void k_wlm_fit(
@@ -535,14 +568,23 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     float* __restrict__ mg, float* __restrict__ vg, float* __restrict__ p_hist,
     float* __restrict__ w_hist, float* __restrict__ t_glob) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int ntab = words * 8;      // one table per nibble of every word (tail nibbles read 0s)
-  const int cols_pad = words * 32;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int ntab = words * 8;        // one table per nibble of every word
+  const int ngrp_alloc = bw * 8;     // g tables cover every nibble of a column word
   const int ngrp = (batch + 3) / 4;
-  float* w_s = reinterpret_cast<float*>(smem);               // [cols_pad]
-  float* g_s = w_s + cols_pad;                                // [ngrp * 4]
-  float* G = g_s + ngrp * 4;                                  // [ngrp * 17]
-  float* T = T_IN_LDS ? (G + ngrp * kTabPitch) : t_glob;      // [words * 8 * 17]
+  float* G = reinterpret_cast<float*>(smem);                         // [ngrp_alloc][17]
+  float* T = T_IN_LDS ? (G + ngrp_alloc * kTabPitch) : t_glob;       // [ntab][17]
+
+  // prediction layout: tpr lanes per mask row (power of 2, <= 16 so a wave holds >= 4 rows)
+  int cap = batch < 1024 ? batch : 1024;
+  int tpr = 16;
+  while (tpr > 1 && 1024 / tpr < cap) tpr >>= 1;
+  const int rpp = 1024 / tpr, rows_w = 64 / tpr, sub = tid & (tpr - 1);
+  const int passes = (batch + rpp - 1) / rpp;
+  const int nw = (words + tpr - 1) / tpr;
+  const bool pf = passes == 1 && nw <= kNW && bw <= kBW;
+  const float l1s = P.l1_lambda / static_cast<float>(cols);
+  const int64_t nsteps = (rows + batch - 1) / batch;
 
   float w[CPT], m[CPT], v[CPT];
 #pragma unroll
@@ -552,45 +594,62 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     m[c] = i < cols ? mg[i] : 0.f;
     v[c] = i < cols ? vg[i] : 0.f;
   }
-  for (int i = tid; i < cols_pad; i += 1024) w_s[i] = i < cols ? wg[i] : 0.f;
-  __syncthreads();
+  for (int e = tid; e < ngrp_alloc * kTabPitch; e += 1024) G[e] = 0.f;
+  wlm_build_T<CPT>(w, T, ntab);
 
-  // threads per mask row in the prediction: power of two, rows x TPR ~ 1024
-  int tpr = 64;
-  while (tpr > 1 && (1024 / tpr) < batch) tpr >>= 1;
-  const int rows_per_pass = 1024 / tpr;
-  const int sub = tid & (tpr - 1);
-  const int passes = (batch + rows_per_pass - 1) / rows_per_pass;
-  const float l1s = P.l1_lambda / static_cast<float>(cols);
-  const int64_t nsteps = (rows + batch - 1) / batch;
+  uint32_t rw[kNW];
+  constexpr int CPF = CPT <= 2 ? CPT : 1;  // columns per thread with prefetched column words
+  uint32_t cw[CPF][kBW];
+  double kv = 0.0;
+#define XPG_LOAD_ROWS(TT)                                                                 \
+  {                                                                                       \
+    const int64_t r0_ = (TT) * batch;                                                     \
+    const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);        \
+    const int j_ = tid / tpr;                                                             \
+    const uint32_t* row_ = bits + (r0_ + (j_ < B_ ? j_ : 0)) * words;                    \
+    _Pragma("unroll") for (int k = 0; k < kNW; ++k) {                                     \
+      const int wd_ = sub + k * tpr;                                                      \
+      rw[k] = (k < nw && wd_ < words && j_ < B_) ? row_[wd_] : 0u;                        \
+    }                                                                                     \
+    kv = j_ < B_ ? kern[r0_ + j_] : 0.0;                                                  \
+  }
+#define XPG_LOAD_COLS(TT)                                                                 \
+  {                                                                                       \
+    _Pragma("unroll") for (int c = 0; c < CPF; ++c) {                                     \
+      const int i_ = tid + c * 1024;                                                      \
+      const uint32_t* cb_ = colbits + ((TT) * cols + (i_ < cols ? i_ : 0)) * bw;          \
+      _Pragma("unroll") for (int k = 0; k < kBW; ++k) cw[c][k] = (k < bw && i_ < cols) ? cb_[k] : 0u; \
+    }                                                                                     \
+  }
+  const bool pfc = pf && CPT <= 2;
+  if (pf) XPG_LOAD_ROWS(0)
+  if (pfc) XPG_LOAD_COLS(0)
+  __syncthreads();
 
   for (int64_t t = 0; t < nsteps; ++t) {
     const int64_t r0 = t * batch;
     const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
     const WlmStep sc = stp[t];
-    // A: nibble tables of w; record the pre-step weights (loss regulariser term)
-    for (int e = tid; e < ntab * 16; e += 1024) {
-      const int tb = e >> 4, vv = e & 15;
-      const float* wb = w_s + tb * 4;
-      float s = 0.f;
-      s += (vv & 1) ? wb[0] : 0.f;
-      s += (vv & 2) ? wb[1] : 0.f;
-      s += (vv & 4) ? wb[2] : 0.f;
-      s += (vv & 8) ? wb[3] : 0.f;
-      T[tb * kTabPitch + vv] = s;
-    }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int i = tid + c * 1024;
       if (i < cols) w_hist[t * cols + i] = w[c];
     }
-    __syncthreads();
-    if (!T_IN_LDS) __threadfence_block();
-    // B: predictions p_j = M_b[j] . w, then g_j = 2 k_j (p_j - ybar) / (B sum k)
+    // ---- predictions p_j = M_b[j] . w and g_j; nibble tables of g built inside each wave
     for (int ps = 0; ps < passes; ++ps) {
-      const int j = ps * rows_per_pass + tid / tpr;
+      const int j = ps * rpp + tid / tpr;
       float s = 0.f;
-      if (j < B) {
+      if (pf) {
+#pragma unroll
+        for (int k = 0; k < kNW; ++k) {
+          if (k < nw) {
+            const uint32_t word = rw[k];
+            const float* tw = T + ((sub + k * tpr) * 8) * kTabPitch;
+#pragma unroll 2
+            for (int nb = 0; nb < 8; ++nb) s += tw[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
+          }
+        }
+      } else if (j < B) {
         const uint32_t* row = bits + (r0 + j) * words;
         for (int wd = sub; wd < words; wd += tpr) {
           const uint32_t word = row[wd];
@@ -600,43 +659,56 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
         }
       }
       for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      if (sub == 0 && j < ngrp * 4) {
-        float g = 0.f;
-        if (j < B) {
-          p_hist[r0 + j] = s;
-          const double kj = kern[r0 + j];
-          g = static_cast<float>(2.0 * kj * (static_cast<double>(s) - sc.ybar) /
-                                 (static_cast<double>(B) * sc.ksum));
+      float g = 0.f;
+      if (j < B) {
+        if (sub == 0) p_hist[r0 + j] = s;
+        const double kj = pf ? kv : kern[r0 + j];
+        g = static_cast<float>(2.0 * kj * (static_cast<double>(s) - sc.ybar) /
+                               (static_cast<double>(B) * sc.ksum));
+      }
+      const int jw0 = ps * rpp + (tid >> 6) * rows_w;  // first batch row held by this wave
+      const int ent_w = rows_w * 4;                    // 16 entries per 4-row group
+      for (int e0 = 0; e0 < ent_w; e0 += 64) {
+        const int e = e0 + lane;
+        const int gl = e >> 4, vv = e & 15;
+        float acc = 0.f;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          int src = 4 * gl + b;
+          src = src < rows_w ? src : rows_w - 1;
+          const float gb = __shfl(g, src * tpr, 64);
+          acc += ((vv >> b) & 1) ? gb : 0.f;
         }
-        g_s[j] = g;
+        const int grp = (jw0 >> 2) + gl;
+        if (e < ent_w && grp < ngrp) G[grp * kTabPitch + vv] = acc;
       }
     }
+    if (pf && t + 1 < nsteps) XPG_LOAD_ROWS(t + 1)
     __syncthreads();
-    // C: nibble tables of g over groups of 4 rows
-    for (int e = tid; e < ngrp * 16; e += 1024) {
-      const int gr = e >> 4, vv = e & 15;
-      const float* gb = g_s + gr * 4;
-      float s = 0.f;
-      s += (vv & 1) ? gb[0] : 0.f;
-      s += (vv & 2) ? gb[1] : 0.f;
-      s += (vv & 4) ? gb[2] : 0.f;
-      s += (vv & 8) ? gb[3] : 0.f;
-      G[gr * kTabPitch + vv] = s;
-    }
-    __syncthreads();
-    // D: gradient M_b^T g + L1 subgradient + L2 decay, Adam (torch single-tensor order)
+    // ---- gradient M_b^T g + L1 subgradient + L2 decay; Adam (torch single-tensor order)
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int i = tid + c * 1024;
       if (i < cols) {
-        const uint32_t* cb = colbits + (t * cols + i) * bw;
         float s = 0.f;
-        for (int jw = 0; jw < bw; ++jw) {
-          const uint32_t word = cb[jw];
-          const int g0 = jw * 8;
+        if (pfc) {
 #pragma unroll
-          for (int nb = 0; nb < 8; ++nb)
-            if (g0 + nb < ngrp) s += G[(g0 + nb) * kTabPitch + ((word >> (4 * nb)) & 15u)];
+          for (int k = 0; k < kBW; ++k) {
+            if (k < bw) {
+              const uint32_t word = cw[c < CPF ? c : 0][k];
+              const float* gk = G + (k * 8) * kTabPitch;
+#pragma unroll 2
+              for (int nb = 0; nb < 8; ++nb) s += gk[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
+            }
+          }
+        } else {
+          const uint32_t* cb = colbits + (t * cols + i) * bw;
+          for (int k = 0; k < bw; ++k) {
+            const uint32_t word = cb[k];
+            const float* gk = G + (k * 8) * kTabPitch;
+#pragma unroll
+            for (int nb = 0; nb < 8; ++nb) s += gk[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
+          }
         }
         const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
         float g = fmaf(l1s, sg, s);
@@ -645,9 +717,10 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
         v[c] = fmaf(1.f - P.beta2, g * g, v[c] * P.beta2);
         const float denom = sqrtf(v[c]) / sc.bc2_sqrt + P.eps;
         w[c] = w[c] - sc.step_size * (m[c] / denom);
-        w_s[i] = w[c];
       }
     }
+    if (pfc && t + 1 < nsteps) XPG_LOAD_COLS(t + 1)
+    wlm_build_T<CPT>(w, T, ntab);
     __syncthreads();
   }
 #pragma unroll
@@ -659,6 +732,8 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       vg[i] = v[c];
     }
   }
+#undef XPG_LOAD_ROWS
+#undef XPG_LOAD_COLS
 }
 
 // loss_t = sum_j k_j (p_j - ybar)^2 / (B sum k) + sum_i (y_i - ybar)^2 / B^2 + l1 * mean|w_t|
@@ -842,8 +917,12 @@ int xpg_shap_kernel(const int32_t* counts, int64_t rows, int64_t cols, double* k
   if (cols - 1 <= 1000)
     hipLaunchKernelGGL(k_shap_exact, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream), counts,
                        rows, cols, kernel_out);
-  else
-    hipLaunchKernelGGL(k_shap, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
+  else {
+    hipLaunchKernelGGL(k_shap_approx_rows, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream),
+                       counts, rows, cols, kernel_out);
+    XPG_LAUNCHED();
+    hipLaunchKernelGGL(k_shap_approx_finish, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
+  }
   XPG_LAUNCHED();
   return XPG_OK;
 }
@@ -962,8 +1041,7 @@ static int wlm_layout(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
   const int64_t steps = cdiv(rows, batch);
   const int words = words_of(cols);
   L->bw = static_cast<int>(cdiv(batch, 32));
-  const int64_t ngrp = cdiv(batch, 4);
-  const size_t base_lds = sizeof(float) * (size_t)((int64_t)words * 32 + ngrp * 4 + ngrp * kTabPitch);
+  const size_t base_lds = sizeof(float) * (size_t)(L->bw * 8 * kTabPitch);
   const size_t t_bytes = sizeof(float) * (size_t)words * 8 * kTabPitch;
   XPG_REQ(base_lds <= 150 * 1024, "wlm_fit: batch x columns too large for the single-workgroup fit (LDS)");
   L->t_in_lds = base_lds + t_bytes <= 150 * 1024;

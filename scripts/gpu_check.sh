@@ -19,6 +19,6 @@ for step in "$@"; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
-           run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+           run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
   esac
 done
