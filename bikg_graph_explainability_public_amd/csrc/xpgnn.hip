@@ -530,8 +530,7 @@ __global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict_
 }
 
 constexpr int kTabPitch = 17;  // 16 entries + 1 pad (bank spread across tables)
-constexpr int kNW = 12;        // prefetched mask words per thread (prediction)
-constexpr int kBW = 8;         // prefetched column words per owned column (gradient, B <= 256)
+constexpr int kStage = 16;     // staged words per thread per buffer (buffer <= 16K words)
 
 // In-wave rebuild of the w nibble tables: the 4 columns of table g are owned by 4 adjacent
 // lanes (column i = tid + 1024 c), so each lane shuffles its group's 4 weights and writes 4 of
@@ -560,7 +559,17 @@ __device__ __forceinline__ void wlm_build_T(const float (&w)[CPT], float* T, int
   }
 }
 
-template <int CPT, bool T_IN_LDS>
+__device__ __forceinline__ float nib8(const float* tab, uint32_t word) {
+  float a[8];
+#pragma unroll
+  for (int nb = 0; nb < 8; ++nb) a[nb] = tab[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// STAGE: the step's mask rows ([B][words], pitch rp) and column bit vectors ([cols][bw], pitch
+// cp) live in LDS; the next step's copies are loaded into registers right after a barrier and
+// written to LDS just before the next one, so their global latency hides behind a phase.
+template <int CPT, bool STAGE>
 __global__ __launch_bounds__(1024) void k_wlm_fit(
     const uint32_t* __restrict__ bits, const uint32_t* __restrict__ colbits, int64_t rows,
     int cols, int words, int batch, int bw, const double* __restrict__ kern,
@@ -572,8 +581,11 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
   const int ntab = words * 8;        // one table per nibble of every word
   const int ngrp_alloc = bw * 8;     // g tables cover every nibble of a column word
   const int ngrp = (batch + 3) / 4;
+  const int rp = words | 1, cp = bw | 1;
   float* G = reinterpret_cast<float*>(smem);                         // [ngrp_alloc][17]
-  float* T = T_IN_LDS ? (G + ngrp_alloc * kTabPitch) : t_glob;       // [ntab][17]
+  float* T = STAGE ? (G + ngrp_alloc * kTabPitch) : t_glob;          // [ntab][17]
+  uint32_t* Rb = reinterpret_cast<uint32_t*>(T + ntab * kTabPitch);  // STAGE: [batch][rp]
+  uint32_t* Cb = Rb + batch * rp;                                     // STAGE: [cols][cp]
 
   // prediction layout: tpr lanes per mask row (power of 2, <= 16 so a wave holds >= 4 rows)
   int cap = batch < 1024 ? batch : 1024;
@@ -581,8 +593,6 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
   while (tpr > 1 && 1024 / tpr < cap) tpr >>= 1;
   const int rpp = 1024 / tpr, rows_w = 64 / tpr, sub = tid & (tpr - 1);
   const int passes = (batch + rpp - 1) / rpp;
-  const int nw = (words + tpr - 1) / tpr;
-  const bool pf = passes == 1 && nw <= kNW && bw <= kBW;
   const float l1s = P.l1_lambda / static_cast<float>(cols);
   const int64_t nsteps = (rows + batch - 1) / batch;
 
@@ -597,39 +607,54 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
   for (int e = tid; e < ngrp_alloc * kTabPitch; e += 1024) G[e] = 0.f;
   wlm_build_T<CPT>(w, T, ntab);
 
-  uint32_t rw[kNW];
-  constexpr int CPF = CPT <= 2 ? CPT : 1;  // columns per thread with prefetched column words
-  uint32_t cw[CPF][kBW];
-  double kv = 0.0;
-#define XPG_LOAD_ROWS(TT)                                                                 \
-  {                                                                                       \
-    const int64_t r0_ = (TT) * batch;                                                     \
-    const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);        \
-    const int j_ = tid / tpr;                                                             \
-    const uint32_t* row_ = bits + (r0_ + (j_ < B_ ? j_ : 0)) * words;                    \
-    _Pragma("unroll") for (int k = 0; k < kNW; ++k) {                                     \
-      const int wd_ = sub + k * tpr;                                                      \
-      rw[k] = (k < nw && wd_ < words && j_ < B_) ? row_[wd_] : 0u;                        \
-    }                                                                                     \
-    kv = j_ < B_ ? kern[r0_ + j_] : 0.0;                                                  \
+  uint32_t stg[kStage];
+  // stage-load helpers (flat element index q*1024 + tid over the buffer's logical extent)
+#define XPG_ROWS_LOAD(TT)                                                               \
+  {                                                                                     \
+    const int64_t r0_ = (TT) * batch;                                                   \
+    const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);      \
+    const uint32_t* src_ = bits + r0_ * words;                                          \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      stg[q] = e_ < B_ * words ? src_[e_] : 0u;                                         \
+    }                                                                                   \
   }
-#define XPG_LOAD_COLS(TT)                                                                 \
-  {                                                                                       \
-    _Pragma("unroll") for (int c = 0; c < CPF; ++c) {                                     \
-      const int i_ = tid + c * 1024;                                                      \
-      const uint32_t* cb_ = colbits + ((TT) * cols + (i_ < cols ? i_ : 0)) * bw;          \
-      _Pragma("unroll") for (int k = 0; k < kBW; ++k) cw[c][k] = (k < bw && i_ < cols) ? cb_[k] : 0u; \
-    }                                                                                     \
+#define XPG_ROWS_STORE()                                                                \
+  {                                                                                     \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      if (e_ < batch * words) Rb[(e_ / words) * rp + (e_ % words)] = stg[q];            \
+    }                                                                                   \
   }
-  const bool pfc = pf && CPT <= 2;
-  if (pf) XPG_LOAD_ROWS(0)
-  if (pfc) XPG_LOAD_COLS(0)
+#define XPG_COLS_LOAD(TT)                                                               \
+  {                                                                                     \
+    const uint32_t* src_ = colbits + (TT) * cols * bw;                                  \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      stg[q] = e_ < cols * bw ? src_[e_] : 0u;                                          \
+    }                                                                                   \
+  }
+#define XPG_COLS_STORE()                                                                \
+  {                                                                                     \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      if (e_ < cols * bw) Cb[(e_ / bw) * cp + (e_ % bw)] = stg[q];                      \
+    }                                                                                   \
+  }
+  // schedule: Cb(t) is loaded at the start of phase B(t) and stored before barrier 1 (the
+  // previous reader, D(t-1), finished at barrier 2); Rb(t+1) is loaded at the start of D(t)
+  // and stored before barrier 2 (its previous reader, B(t), finished at barrier 1).
+  if (STAGE) {
+    XPG_ROWS_LOAD(0)
+    XPG_ROWS_STORE()
+  }
   __syncthreads();
 
   for (int64_t t = 0; t < nsteps; ++t) {
     const int64_t r0 = t * batch;
     const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
     const WlmStep sc = stp[t];
+    if (STAGE) XPG_COLS_LOAD(t)
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int i = tid + c * 1024;
@@ -639,30 +664,22 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     for (int ps = 0; ps < passes; ++ps) {
       const int j = ps * rpp + tid / tpr;
       float s = 0.f;
-      if (pf) {
-#pragma unroll
-        for (int k = 0; k < kNW; ++k) {
-          if (k < nw) {
-            const uint32_t word = rw[k];
-            const float* tw = T + ((sub + k * tpr) * 8) * kTabPitch;
+      if (j < B) {
+        if (STAGE) {
+          const uint32_t* row = Rb + j * rp;
 #pragma unroll 2
-            for (int nb = 0; nb < 8; ++nb) s += tw[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
-          }
-        }
-      } else if (j < B) {
-        const uint32_t* row = bits + (r0 + j) * words;
-        for (int wd = sub; wd < words; wd += tpr) {
-          const uint32_t word = row[wd];
-          const float* tw = T + (wd * 8) * kTabPitch;
-#pragma unroll
-          for (int nb = 0; nb < 8; ++nb) s += tw[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
+          for (int wd = sub; wd < words; wd += tpr) s += nib8(T + (wd * 8) * kTabPitch, row[wd]);
+        } else {
+          const uint32_t* row = bits + (r0 + j) * words;
+#pragma unroll 2
+          for (int wd = sub; wd < words; wd += tpr) s += nib8(T + (wd * 8) * kTabPitch, row[wd]);
         }
       }
       for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
       float g = 0.f;
       if (j < B) {
         if (sub == 0) p_hist[r0 + j] = s;
-        const double kj = pf ? kv : kern[r0 + j];
+        const double kj = kern[r0 + j];
         g = static_cast<float>(2.0 * kj * (static_cast<double>(s) - sc.ybar) /
                                (static_cast<double>(B) * sc.ksum));
       }
@@ -683,33 +700,18 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
         if (e < ent_w && grp < ngrp) G[grp * kTabPitch + vv] = acc;
       }
     }
-    if (pf && t + 1 < nsteps) XPG_LOAD_ROWS(t + 1)
-    __syncthreads();
+    if (STAGE) XPG_COLS_STORE()
+    __syncthreads();  // G and Cb(t) complete; Rb free
+    if (STAGE && t + 1 < nsteps) XPG_ROWS_LOAD(t + 1)
     // ---- gradient M_b^T g + L1 subgradient + L2 decay; Adam (torch single-tensor order)
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int i = tid + c * 1024;
       if (i < cols) {
         float s = 0.f;
-        if (pfc) {
-#pragma unroll
-          for (int k = 0; k < kBW; ++k) {
-            if (k < bw) {
-              const uint32_t word = cw[c < CPF ? c : 0][k];
-              const float* gk = G + (k * 8) * kTabPitch;
+        const uint32_t* cb = STAGE ? (Cb + i * cp) : (colbits + (t * cols + i) * bw);
 #pragma unroll 2
-              for (int nb = 0; nb < 8; ++nb) s += gk[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
-            }
-          }
-        } else {
-          const uint32_t* cb = colbits + (t * cols + i) * bw;
-          for (int k = 0; k < bw; ++k) {
-            const uint32_t word = cb[k];
-            const float* gk = G + (k * 8) * kTabPitch;
-#pragma unroll
-            for (int nb = 0; nb < 8; ++nb) s += gk[nb * kTabPitch + ((word >> (4 * nb)) & 15u)];
-          }
-        }
+        for (int k = 0; k < bw; ++k) s += nib8(G + (k * 8) * kTabPitch, cb[k]);
         const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
         float g = fmaf(l1s, sg, s);
         g = fmaf(P.weight_decay, w[c], g);
@@ -719,8 +721,8 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
         w[c] = w[c] - sc.step_size * (m[c] / denom);
       }
     }
-    if (pfc && t + 1 < nsteps) XPG_LOAD_COLS(t + 1)
     wlm_build_T<CPT>(w, T, ntab);
+    if (STAGE && t + 1 < nsteps) XPG_ROWS_STORE()
     __syncthreads();
   }
 #pragma unroll
@@ -732,8 +734,10 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       vg[i] = v[c];
     }
   }
-#undef XPG_LOAD_ROWS
-#undef XPG_LOAD_COLS
+#undef XPG_ROWS_LOAD
+#undef XPG_ROWS_STORE
+#undef XPG_COLS_LOAD
+#undef XPG_COLS_STORE
 }
 
 // loss_t = sum_j k_j (p_j - ybar)^2 / (B sum k) + sum_i (y_i - ybar)^2 / B^2 + l1 * mean|w_t|
@@ -1030,7 +1034,7 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
 struct WlmWs {
   size_t steps_off, colbits_off, phist_off, whist_off, tglob_off, total;
   int bw;
-  bool t_in_lds;
+  bool stage;
   size_t lds;
 };
 
@@ -1041,11 +1045,14 @@ static int wlm_layout(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
   const int64_t steps = cdiv(rows, batch);
   const int words = words_of(cols);
   L->bw = static_cast<int>(cdiv(batch, 32));
-  const size_t base_lds = sizeof(float) * (size_t)(L->bw * 8 * kTabPitch);
+  const size_t g_bytes = sizeof(float) * (size_t)(L->bw * 8 * kTabPitch);
   const size_t t_bytes = sizeof(float) * (size_t)words * 8 * kTabPitch;
-  XPG_REQ(base_lds <= 150 * 1024, "wlm_fit: batch x columns too large for the single-workgroup fit (LDS)");
-  L->t_in_lds = base_lds + t_bytes <= 150 * 1024;
-  L->lds = base_lds + (L->t_in_lds ? t_bytes : 0);
+  const size_t stage_bytes = sizeof(uint32_t) * ((size_t)batch * (words | 1) + (size_t)cols * (L->bw | 1));
+  const size_t lds_cap = 150 * 1024;
+  XPG_REQ(g_bytes <= lds_cap, "wlm_fit: batch too large for the single-workgroup fit (LDS)");
+  L->stage = g_bytes + t_bytes + stage_bytes <= lds_cap && (int64_t)batch * words <= kStage * 1024 &&
+             cols * (int64_t)L->bw <= kStage * 1024;
+  L->lds = g_bytes + (L->stage ? t_bytes + stage_bytes : 0);
   size_t off = 0;
   L->steps_off = off;
   off += align_up(sizeof(WlmStep) * (size_t)steps);
@@ -1056,7 +1063,7 @@ static int wlm_layout(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
   L->whist_off = off;
   off += align_up(sizeof(float) * (size_t)steps * cols);
   L->tglob_off = off;
-  off += align_up(L->t_in_lds ? 0 : t_bytes);
+  off += align_up(L->stage ? 0 : t_bytes);
   L->total = off;
   return XPG_OK;
 }
@@ -1097,7 +1104,7 @@ int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
   XPG_LAUNCHED();
   const int cpt = static_cast<int>(cdiv(cols, 1024));
 #define XPG_WLM(C, TL)                                                                                     \
-  if (cpt <= C && L.t_in_lds == TL) {                                                                      \
+  if (cpt <= C && L.stage == TL) {                                                                      \
     XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit<C, TL>),                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds)));     \
     hipLaunchKernelGGL((k_wlm_fit<C, TL>), dim3(1), dim3(1024), L.lds, st, bits, colbits, rows, ic, words, \
