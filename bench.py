@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--interpret-samples", type=int, default=256)
     p.add_argument("--epochs", type=int, default=50)
     p.add_argument("--query", type=int, default=7)
+    p.add_argument("--repeats", type=int, default=1,
+                   help="Explainer.run(times=...) repeats per rank per step (batched fits)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=12800)
     return p.parse_args()
@@ -146,16 +148,18 @@ def main():
     S = plan.cols
     R = args.interpret_samples * args.epochs
     batch = R // args.epochs
-    w0 = torch.zeros(S, device=dev)
     params = {"lr": 0.01, "l1_lambda": 1e-4}
     stream = torch.cuda.current_stream()
     ev = {k: [] for k in ("sample", "forward", "shap", "wlm")}
+
+    T = args.repeats
+    w0 = torch.zeros((T, S), device=dev)
 
     def step(i, record):
         marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
         if record:
             marks[0].record(stream)
-        bits = engine.sample_shapley(1000 + i * world + rank, R, S, dev)
+        bits = engine.sample_shapley(1000 + i * world + rank, T * R, S, dev)
         if record:
             marks[1].record(stream)
         y = plan.forward(bits)[:, 0]
@@ -164,7 +168,9 @@ def main():
         k = engine.shap_kernel(bits, S)
         if record:
             marks[3].record(stream)
-        w, _, _, _, _ = engine.wlm_fit(bits, S, batch, y, k, w0, params)
+        w, _, _, _, _ = engine.wlm_fit(bits.view(T, R, -1), S, batch, y.view(T, R),
+                                       k.view(T, R), w0, params)
+        w = w.mean(0)
         if record:
             marks[4].record(stream)
             for j, name in enumerate(("sample", "forward", "shap", "wlm")):
@@ -198,19 +204,19 @@ def main():
     phase_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
 
     if rank == 0:
-        total_rows = R * world * args.steps
+        total_rows = R * T * world * args.steps
         dominant = max(phase_ms, key=phase_ms.get)
         if dominant == "wlm":
-            bytes_launch = wlm_bytes(R, S, batch)
+            bytes_launch = wlm_bytes(R, S, batch) * T
             kname = "k_wlm (surrogate Adam loop, 1 persistent workgroup)"
         elif dominant == "forward":
-            bytes_launch = forward_bytes(plan, R)
+            bytes_launch = forward_bytes(plan, R * T)
             kname = "masked forward chain (k_degree + k_agg + k_dense + k_take_col)"
         elif dominant == "shap":
-            bytes_launch = R * ((S + 31) // 32) * 4 + R * 12
+            bytes_launch = T * R * (((S + 31) // 32) * 4 + 12)
             kname = "k_popcount + k_shap"
         else:
-            bytes_launch = R * ((S + 31) // 32) * 4
+            bytes_launch = T * R * ((S + 31) // 32) * 4
             kname = "k_shapley"
         achieved = bytes_launch / (phase_ms[dominant] * 1e-3) / 1e9
         line = {
@@ -232,7 +238,8 @@ def main():
                        "nodes": args.nodes, "edges": args.edges, "feat": args.feat,
                        "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
                        "interpret_samples": args.interpret_samples, "epochs": args.epochs,
-                       "rows_per_repeat": R, "repeats_per_step": world,
+                       "rows_per_repeat": R, "repeats_per_rank": T,
+                       "repeats_per_step": T * world,
                        "parallelism": f"repeats sharded over {world} rank(s)",
                        "mask_sampler": "device (Philox Shapley)"},
             "phases_ms": phase_ms,

@@ -472,6 +472,10 @@ __global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
                                                    WlmStep* __restrict__ st) {
   __shared__ double red[16];
   const int64_t t = blockIdx.x;
+  const int64_t fit = blockIdx.y;
+  y += fit * rows;
+  kern += fit * rows;
+  st += fit * (int64_t)gridDim.x;
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
   double sy = 0.0, sk = 0.0;
@@ -508,8 +512,12 @@ __global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict_
                                                      int64_t steps, uint32_t* __restrict__ colbits) {
   const int lane = threadIdx.x & 63;
   const int chunks = (batch + 63) / 64;
-  const int64_t wave = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (wave >= steps * words * chunks) return;  // wave-uniform exit
+  int64_t wave = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t per_fit = steps * words * chunks;
+  const int64_t fit = blockIdx.y;
+  if (wave >= per_fit) return;  // wave-uniform exit
+  bits += fit * rows * words;
+  colbits += fit * steps * cols * bw;
   const int64_t t = wave / ((int64_t)words * chunks);
   const int rem = static_cast<int>(wave - t * words * chunks);
   const int wd = rem / chunks, ch = rem - wd * chunks;
@@ -529,8 +537,22 @@ __global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict_
   }
 }
 
+#ifdef XPG_WLM_STAMPS  // diagnostic build only (tools/wlm_probe.cpp): per-phase cycle counts
+#define XPG_STAMP(k)                                                       \
+  {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();                    \
+    stamp_acc[k] += now_ - stamp_last;                                     \
+    stamp_last = now_;                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+  }
+__device__ uint64_t g_wlm_stamps[2][8];
+#else
+#define XPG_STAMP(k)
+#endif
+
 constexpr int kTabPitch = 17;  // 16 entries + 1 pad (bank spread across tables)
-constexpr int kStage = 16;     // staged words per thread per buffer (buffer <= 16K words)
+constexpr int kStage = 12;     // staged words per thread per buffer (buffer <= 12K words)
 
 // In-wave rebuild of the w nibble tables: the 4 columns of table g are owned by 4 adjacent
 // lanes (column i = tid + 1024 c), so each lane shuffles its group's 4 weights and writes 4 of
@@ -579,6 +601,21 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int ntab = words * 8;        // one table per nibble of every word
+  {  // independent fits: one workgroup each, fit-major arrays
+    const int64_t f = blockIdx.x;
+    const int64_t st_ = (rows + batch - 1) / batch;
+    const int bw_ = (batch + 31) / 32;
+    bits += f * rows * words;
+    colbits += f * st_ * cols * bw_;
+    kern += f * rows;
+    stp += f * st_;
+    wg += f * cols;
+    mg += f * cols;
+    vg += f * cols;
+    p_hist += f * rows;
+    w_hist += f * st_ * cols;
+    if (t_glob) t_glob += f * (int64_t)ntab * 17;
+  }
   const int ngrp_alloc = bw * 8;     // g tables cover every nibble of a column word
   const int ngrp = (batch + 3) / 4;
   const int rp = words | 1, cp = bw | 1;
@@ -616,7 +653,9 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     const uint32_t* src_ = bits + r0_ * words;                                          \
     _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
       const int e_ = q * 1024 + tid;                                                    \
-      stg[q] = e_ < B_ * words ? src_[e_] : 0u;                                         \
+      const int n_ = B_ * words;                                                        \
+      const uint32_t x_ = src_[e_ < n_ ? e_ : n_ - 1];                                  \
+      stg[q] = e_ < n_ ? x_ : 0u;                                                       \
     }                                                                                   \
   }
 #define XPG_ROWS_STORE()                                                                \
@@ -631,7 +670,8 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     const uint32_t* src_ = colbits + (TT) * cols * bw;                                  \
     _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
       const int e_ = q * 1024 + tid;                                                    \
-      stg[q] = e_ < cols * bw ? src_[e_] : 0u;                                          \
+      const uint32_t x_ = src_[e_ < cols * bw ? e_ : cols * bw - 1];                    \
+      stg[q] = e_ < cols * bw ? x_ : 0u;                                                \
     }                                                                                   \
   }
 #define XPG_COLS_STORE()                                                                \
@@ -649,6 +689,10 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     XPG_ROWS_STORE()
   }
   __syncthreads();
+#ifdef XPG_WLM_STAMPS
+  uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int64_t t = 0; t < nsteps; ++t) {
     const int64_t r0 = t * batch;
@@ -667,14 +711,27 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       if (j < B) {
         if (STAGE) {
           const uint32_t* row = Rb + j * rp;
-#pragma unroll 2
-          for (int wd = sub; wd < words; wd += tpr) s += nib8(T + (wd * 8) * kTabPitch, row[wd]);
+          for (int k0 = 0; k0 * tpr < words; k0 += 4) {
+            uint32_t wv[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const int wd = sub + (k0 + h) * tpr;
+              wv[h] = row[wd < words ? wd : 0];
+            }
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const int wd = sub + (k0 + h) * tpr;
+              const float x = nib8(T + ((wd < words ? wd : 0) * 8) * kTabPitch, wv[h]);
+              s += wd < words ? x : 0.f;
+            }
+          }
         } else {
           const uint32_t* row = bits + (r0 + j) * words;
 #pragma unroll 2
           for (int wd = sub; wd < words; wd += tpr) s += nib8(T + (wd * 8) * kTabPitch, row[wd]);
         }
       }
+      XPG_STAMP(0)
       for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
       float g = 0.f;
       if (j < B) {
@@ -700,8 +757,11 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
         if (e < ent_w && grp < ngrp) G[grp * kTabPitch + vv] = acc;
       }
     }
+    XPG_STAMP(1)
     if (STAGE) XPG_COLS_STORE()
+    XPG_STAMP(2)
     __syncthreads();  // G and Cb(t) complete; Rb free
+    XPG_STAMP(3)
     if (STAGE && t + 1 < nsteps) XPG_ROWS_LOAD(t + 1)
     // ---- gradient M_b^T g + L1 subgradient + L2 decay; Adam (torch single-tensor order)
 #pragma unroll
@@ -710,8 +770,16 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       if (i < cols) {
         float s = 0.f;
         const uint32_t* cb = STAGE ? (Cb + i * cp) : (colbits + (t * cols + i) * bw);
-#pragma unroll 2
-        for (int k = 0; k < bw; ++k) s += nib8(G + (k * 8) * kTabPitch, cb[k]);
+        for (int k0 = 0; k0 < bw; k0 += 4) {
+          uint32_t wv[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) wv[h] = cb[k0 + h < bw ? k0 + h : 0];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const float x = nib8(G + ((k0 + h < bw ? k0 + h : 0) * 8) * kTabPitch, wv[h]);
+            s += k0 + h < bw ? x : 0.f;
+          }
+        }
         const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
         float g = fmaf(l1s, sg, s);
         g = fmaf(P.weight_decay, w[c], g);
@@ -721,10 +789,19 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
         w[c] = w[c] - sc.step_size * (m[c] / denom);
       }
     }
+    XPG_STAMP(4)
     wlm_build_T<CPT>(w, T, ntab);
+    XPG_STAMP(5)
     if (STAGE && t + 1 < nsteps) XPG_ROWS_STORE()
+    XPG_STAMP(6)
     __syncthreads();
+    XPG_STAMP(7)
   }
+#ifdef XPG_WLM_STAMPS
+  if (tid == 0 || tid == 1023) {
+    for (int k = 0; k < 8; ++k) g_wlm_stamps[tid == 0 ? 0 : 1][k] = stamp_acc[k];
+  }
+#endif
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     const int i = tid + c * 1024;
@@ -749,6 +826,14 @@ __global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hi
                                                   double* __restrict__ losses) {
   __shared__ double red[16];
   const int64_t t = blockIdx.x;
+  {
+    const int64_t f = blockIdx.y, steps = gridDim.x;
+    p_hist += f * rows;
+    w_hist += f * steps * cols;
+    kern += f * rows;
+    stp += f * steps;
+    losses += f * steps;
+  }
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
   const WlmStep sc = stp[t];
@@ -768,7 +853,9 @@ __global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hi
 }
 
 __global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (threadIdx.x != 0) return;
+  v += blockIdx.x * n;
+  out += blockIdx.x;
   double best = INFINITY;
   int32_t bi = 0;
   for (int64_t i = 0; i < n; ++i)
@@ -1038,8 +1125,8 @@ struct WlmWs {
   size_t lds;
 };
 
-static int wlm_layout(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
-  XPG_REQ(rows > 0 && cols > 0 && batch > 0, "wlm_fit: bad arguments");
+static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
+  XPG_REQ(n_fits > 0 && rows > 0 && cols > 0 && batch > 0, "wlm_fit: bad arguments");
   XPG_REQ(cols <= 16 * 1024, "wlm_fit: more than 16384 columns is not supported by the single-workgroup fit");
   XPG_REQ(batch <= 1 << 20, "wlm_fit: batch too large");
   const int64_t steps = cdiv(rows, batch);
@@ -1053,36 +1140,38 @@ static int wlm_layout(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
   L->stage = g_bytes + t_bytes + stage_bytes <= lds_cap && (int64_t)batch * words <= kStage * 1024 &&
              cols * (int64_t)L->bw <= kStage * 1024;
   L->lds = g_bytes + (L->stage ? t_bytes + stage_bytes : 0);
+  const size_t F = static_cast<size_t>(n_fits);
   size_t off = 0;
   L->steps_off = off;
-  off += align_up(sizeof(WlmStep) * (size_t)steps);
+  off += align_up(F * sizeof(WlmStep) * (size_t)steps);
   L->colbits_off = off;
-  off += align_up(sizeof(uint32_t) * (size_t)steps * cols * L->bw);
+  off += align_up(F * sizeof(uint32_t) * (size_t)steps * cols * L->bw);
   L->phist_off = off;
-  off += align_up(sizeof(float) * (size_t)rows);
+  off += align_up(F * sizeof(float) * (size_t)rows);
   L->whist_off = off;
-  off += align_up(sizeof(float) * (size_t)steps * cols);
+  off += align_up(F * sizeof(float) * (size_t)steps * cols);
   L->tglob_off = off;
-  off += align_up(L->stage ? 0 : t_bytes);
+  off += align_up(L->stage ? 0 : F * t_bytes);
   L->total = off;
   return XPG_OK;
 }
 
-int xpg_wlm_workspace(int64_t rows, int64_t cols, int64_t batch, size_t* bytes) {
+int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, size_t* bytes) {
   WlmWs L;
-  int rc = wlm_layout(rows, cols, batch, &L);
+  int rc = wlm_layout(n_fits, rows, cols, batch, &L);
   if (rc) return rc;
   *bytes = L.total;
   return XPG_OK;
 }
 
-int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch, const float* y,
-                const double* kernel, const xpg_wlm_params* params, int64_t step0, float* w,
-                float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, void* workspace,
-                size_t workspace_bytes, xpg_stream_t stream) {
+int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
+                float* w, float* adam_m, float* adam_v, double* losses, int32_t* best_epoch,
+                void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
   XPG_REQ(params != nullptr, "wlm_fit: params required");
+  XPG_REQ(n_fits <= 65535, "wlm_fit: at most 65535 fits per launch");
   WlmWs L;
-  int rc = wlm_layout(rows, cols, batch, &L);
+  int rc = wlm_layout(n_fits, rows, cols, batch, &L);
   if (rc) return rc;
   XPG_REQ(workspace_bytes >= L.total, "wlm_fit: workspace too small");
   hipStream_t st = S(stream);
@@ -1095,19 +1184,20 @@ int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
   const int64_t steps = cdiv(rows, batch);
   const int words = words_of(cols);
   const int ic = static_cast<int>(cols), ib = static_cast<int>(batch);
-  hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps)), dim3(256), 0, st, y, kernel, rows, ib,
+  const unsigned nf = static_cast<unsigned>(n_fits);
+  hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib,
                      *params, step0, stp);
   XPG_LAUNCHED();
   const int64_t waves = steps * words * cdiv(batch, 64);
-  hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(waves, 4))), dim3(256), 0, st, bits, rows, ic,
-                     words, ib, L.bw, steps, colbits);
+  hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(waves, 4)), nf), dim3(256), 0, st, bits, rows,
+                     ic, words, ib, L.bw, steps, colbits);
   XPG_LAUNCHED();
   const int cpt = static_cast<int>(cdiv(cols, 1024));
 #define XPG_WLM(C, TL)                                                                                     \
   if (cpt <= C && L.stage == TL) {                                                                      \
     XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit<C, TL>),                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds)));     \
-    hipLaunchKernelGGL((k_wlm_fit<C, TL>), dim3(1), dim3(1024), L.lds, st, bits, colbits, rows, ic, words, \
+    hipLaunchKernelGGL((k_wlm_fit<C, TL>), dim3(nf), dim3(1024), L.lds, st, bits, colbits, rows, ic, words, \
                        ib, L.bw, kernel, stp, *params, w, adam_m, adam_v, p_hist, w_hist, t_glob);         \
     XPG_LAUNCHED();                                                                                        \
     goto fitted;                                                                                           \
@@ -1117,10 +1207,10 @@ int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
 #undef XPG_WLM
   return fail(XPG_EINVAL, "wlm_fit: unsupported column count");
 fitted:
-  hipLaunchKernelGGL(k_wlm_loss, dim3(static_cast<unsigned>(steps)), dim3(256), 0, st, p_hist, w_hist, kernel,
+  hipLaunchKernelGGL(k_wlm_loss, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, p_hist, w_hist, kernel,
                      stp, rows, ic, ib, params->l1_lambda, losses);
   XPG_LAUNCHED();
-  hipLaunchKernelGGL(k_argmin_first, dim3(1), dim3(64), 0, st, losses, steps, best_epoch);
+  hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch);
   XPG_LAUNCHED();
   return XPG_OK;
 }

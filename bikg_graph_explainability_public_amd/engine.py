@@ -313,27 +313,36 @@ def _workspace(dev, nbytes):
 
 
 def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0):
-    """train_model (wlm.py:132-278) epoch loop on device.  Returns (w, losses, best_epoch,
-    adam_m, adam_v)."""
+    """train_model (wlm.py:132-278) epoch loop on device for one or many independent fits.
+
+    bits [R, W] or [F, R, W]; y / kernel [R] or [F, R]; w0 [S] or [F, S].  Returns
+    (w, losses, best_epoch, adam_m, adam_v) with the same leading fit dimension (if any)."""
     dev = bits.device
-    rows = bits.shape[0]
+    batched = bits.dim() == 3
+    F = bits.shape[0] if batched else 1
+    rows = bits.shape[-2]
     if batch <= 0:
         raise ValueError("batch_size should be a positive integer value, but got "
                          f"batch_size={batch}")
     nsteps = math.ceil(rows / batch)
-    w = w0.detach().to(device=dev, dtype=torch.float32).reshape(-1).clone()
-    m = torch.zeros(cols, dtype=torch.float32, device=dev) if m0 is None else m0.clone()
-    v = torch.zeros(cols, dtype=torch.float32, device=dev) if v0 is None else v0.clone()
-    losses = torch.empty(nsteps, dtype=torch.float64, device=dev)
-    best = torch.empty(1, dtype=torch.int32, device=dev)
+    w = w0.detach().to(device=dev, dtype=torch.float32).reshape(F, cols).clone()
+    m = torch.zeros((F, cols), dtype=torch.float32, device=dev) if m0 is None else \
+        m0.reshape(F, cols).clone()
+    v = torch.zeros((F, cols), dtype=torch.float32, device=dev) if v0 is None else \
+        v0.reshape(F, cols).clone()
+    losses = torch.empty((F, nsteps), dtype=torch.float64, device=dev)
+    best = torch.empty(F, dtype=torch.int32, device=dev)
     p = WlmParams(lr=abs(float(params["lr"])), l1_lambda=float(params["l1_lambda"]), beta1=0.9,
                   beta2=0.999, eps=1e-8, weight_decay=1e-2)
-    yy = y.to(device=dev, dtype=torch.float32).contiguous()
-    kk = kernel.to(device=dev, dtype=torch.float64).contiguous()
+    yy = y.to(device=dev, dtype=torch.float32).reshape(F, rows).contiguous()
+    kk = kernel.to(device=dev, dtype=torch.float64).reshape(F, rows).contiguous()
+    bb = bits.contiguous()
     n = ctypes.c_size_t(0)
-    _lib.check(_lib.load().xpg_wlm_workspace(rows, cols, batch, ctypes.byref(n)))
+    _lib.check(_lib.load().xpg_wlm_workspace(F, rows, cols, batch, ctypes.byref(n)))
     ws = _workspace(dev, n.value)
-    call("xpg_wlm_fit", ptr(bits), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
+    call("xpg_wlm_fit", F, ptr(bb), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
          int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(ws), ws.numel(),
          _lib.stream_of(dev))
+    if not batched:
+        return w[0], losses[0], best[0:1], m[0], v[0]
     return w, losses, best, m, v

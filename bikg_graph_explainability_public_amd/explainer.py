@@ -197,34 +197,42 @@ class Explainer:
 
         sampler = self.params.get("mask_sampler", "compat")
         _, epochs = Mask.assertions_mask_generator(self.params)
-        config_vals, diag = [], []
+        # draw every repeat's masks and initial surrogate weights first, in the reference's
+        # RNG order (mask_generator -> LinearRegression init -> DataLoader seed, per repeat);
+        # then run all repeats' forward / KernelSHAP / surrogate fits as batched launches.
+        bits_list, w0_list, masks = [], [], []
         for _ in range(times):
             if sampler == "device" and c["sub_pw_inds"] is None and "edge" not in self.problem:
                 R = int(self.params["interpret_samples"] * epochs)
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-                bits = engine.sample_shapley(seed, R, S, device)
-                mask = None
+                bits_list.append(engine.sample_shapley(seed, R, S, device))
+                masks.append(None)
             else:
                 mask, _ = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,
                                self.problem).generate()
                 mask = mask.to(device)
-                bits = engine.pack_masks(mask)
-                R = mask.shape[0]
-            wlrm = LinearRegression(S)
+                bits_list.append(engine.pack_masks(mask))
+                masks.append(mask)
+            w0_list.append(LinearRegression(S).layer.weight.detach().reshape(-1))
             dataloader_seed_draw()
-            batch = R // epochs
-            if plan is not None:
-                y = plan.forward(bits)[:, 0]
-            else:
-                if mask is None:
-                    mask = engine.unpack_masks(bits, S)
-                y = pipeline.generic_outputs(self.arch, sub_feat, sub_ei, mask, sub_ind,
-                                             self.problem, *geo, batch=batch)
-            w, losses, best, _ = pipeline.fit_repeat(bits, S, batch, y,
-                                                     wlrm.layer.weight.detach(), self.params)
-            config_vals.append(w)
-            diag.append({"losses": losses, "best_epoch": best, "rows": R, "batch": batch,
-                         "y": y, "bits": bits})
+        R = bits_list[0].shape[0]
+        batch = R // epochs
+        bits = torch.stack(bits_list)                       # [times, R, W]
+        if plan is not None:
+            y = plan.forward(bits.reshape(times * R, -1))[:, 0].reshape(times, R)
+        else:
+            ys = []
+            for b_, m_ in zip(bits_list, masks):
+                m_ = engine.unpack_masks(b_, S) if m_ is None else m_
+                ys.append(pipeline.generic_outputs(self.arch, sub_feat, sub_ei, m_, sub_ind,
+                                                   self.problem, *geo, batch=batch))
+            y = torch.stack(ys)
+        kern = engine.shap_kernel(bits.reshape(times * R, -1), S).reshape(times, R)
+        w, losses, best, _, _ = engine.wlm_fit(bits, S, batch, y, kern,
+                                               torch.stack(w0_list), self.params)
+        config_vals = [w[i] for i in range(times)]
+        diag = [{"losses": losses[i], "best_epoch": best[i], "rows": R, "batch": batch,
+                 "y": y[i], "bits": bits[i]} for i in range(times)]
         mean, std = self.weight_stacking(config_vals)
         config_val_df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
         pathway_df = None

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 2
+#define XPG_ABI_VERSION 3
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -146,15 +146,17 @@ typedef struct xpg_wlm_params {
 } xpg_wlm_params;
 
 /* Workspace needed by xpg_wlm_fit. */
-int xpg_wlm_workspace(int64_t rows, int64_t cols, int64_t batch, size_t* bytes);
-/* Runs ceil(rows / batch) Adam steps of train_model over consecutive row batches; w, m, v are
- * updated in place (fp32 [cols]); losses[step] (fp64) and best_epoch (first argmin) written.
- * `step0` is the number of Adam steps already taken with (m, v) (0 for a fresh optimizer). */
-int xpg_wlm_fit(const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
-                const float* y, const double* kernel, const xpg_wlm_params* params,
-                int64_t step0, float* w, float* adam_m, float* adam_v, double* losses,
-                int32_t* best_epoch, void* workspace, size_t workspace_bytes,
-                xpg_stream_t stream);
+int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, size_t* bytes);
+/* Runs ceil(rows / batch) Adam steps of train_model over consecutive row batches for n_fits
+ * independent surrogates (e.g. the `times` repeats of Explainer.run), one workgroup each.
+ * Arrays are fit-major and contiguous: bits [n_fits][rows][words], y / kernel [n_fits][rows],
+ * w / adam_m / adam_v [n_fits][cols] (updated in place), losses [n_fits][steps] (fp64),
+ * best_epoch [n_fits] (first argmin).  `step0` = Adam steps already taken with (m, v). */
+int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols,
+                int64_t batch, const float* y, const double* kernel,
+                const xpg_wlm_params* params, int64_t step0, float* w, float* adam_m,
+                float* adam_v, double* losses, int32_t* best_epoch, void* workspace,
+                size_t workspace_bytes, xpg_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,8 @@ for step in "$@"; do
     tests) run gpu_tests 900 python -m pytest tests -m gpu -q -rf ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py ;;
+    bench10) run bench10 600 python bench.py --repeats 10 --no-cpu-baseline ;;
+    probe) run probe 120 ./tools/wlm_probe 1193 12800 256 ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
   esac

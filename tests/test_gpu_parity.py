@@ -207,6 +207,26 @@ def test_wlm_fit_vs_oracle_large():
     np.testing.assert_allclose(losses.cpu().numpy(), rl, rtol=1e-5)
 
 
+def test_wlm_fit_batched_independent_fits():
+    """n_fits independent surrogates in one launch (one workgroup each) == separate fits."""
+    e = _eng()
+    rng = np.random.default_rng(5)
+    F, R, S, B = 5, 1002, 200, 20
+    m = rng.random((F, R, S)) < 0.5
+    y = rng.random((F, R)).astype(np.float32)
+    k = np.stack([oracle.shap_kernel(m[f]) for f in range(F)])
+    w0 = ((rng.random((F, S)) - 0.5) * 0.1).astype(np.float32)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    bits = torch.stack([e.pack_masks(torch.as_tensor(m[f]).to(DEV)) for f in range(F)])
+    w, losses, best, _, _ = e.wlm_fit(bits, S, B, torch.as_tensor(y), torch.as_tensor(k),
+                                      torch.as_tensor(w0), params)
+    for f in range(F):
+        ref, rl, rb = oracle.train_wlm(m[f], B, y[f], k[f], w0[f], params)
+        np.testing.assert_allclose(w[f].cpu().numpy(), ref, rtol=0, atol=1e-4)
+        np.testing.assert_allclose(losses[f].cpu().numpy(), rl, rtol=1e-5)
+        assert int(best[f]) == rb
+
+
 # ------------------------------------------------------------------ end to end
 @pytest.mark.parametrize("name", CASES)
 def test_explainer_run_matches_reference_dataframes(name):
