@@ -141,7 +141,7 @@ def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", torch.cuda.current_device())
-    from bikg_graph_explainability_public_amd import _lib, engine
+    from bikg_graph_explainability_public_amd import _lib, engine, sharding
 
     _lib.load()
     arch, sub_feat, sub_ei, q, plan = build_workload(args, dev)
@@ -170,18 +170,14 @@ def main():
             marks[3].record(stream)
         w, _, _, _, _ = engine.wlm_fit(bits.view(T, R, -1), S, batch, y.view(T, R),
                                        k.view(T, R), w0, params)
-        w = w.mean(0)
         if record:
             marks[4].record(stream)
             for j, name in enumerate(("sample", "forward", "shap", "wlm")):
                 ev[name].append((marks[j], marks[j + 1]))
         if world > 1:
-            import torch.distributed as dist
-            out = [torch.empty_like(w) for _ in range(world)]
-            dist.all_gather(out, w)
-            st = torch.stack(out)
-            return st.mean(0), st.std(0, unbiased=False)
-        return w, None
+            # weight_stacking (explainer.py:288-314) over every rank's repeats: one all-gather
+            w = sharding.gather_rows(w.reshape(T, S), T * world)
+        return w.mean(0), w.std(0, unbiased=False)
 
     for i in range(args.warmup):
         step(i, False)

@@ -10,7 +10,9 @@
 // (v_mfma_f32_32x32x2_f32: exact fp32 fma chains, no reduced-precision path).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -449,6 +451,229 @@ __global__ void k_take_col(const float* __restrict__ C, int64_t M, int64_t ldc, 
   if (m < M) y[m] = C[m * ldc + col];
 }
 
+// ------------------------------------------------------------------------------ fused forward
+// The whole masked forward of a small plan (a query's receptive field) in ONE launch: one wave
+// per mask row, lanes = feature chunks.  The layer-1 tables (X W^T of the F_0 nodes) and the
+// weights of layers >= 2 are copied into LDS once per workgroup; the row's mask words, kept
+// in-degrees and layer outputs live in the wave's own LDS slice, so nothing per row touches HBM
+// except the mask words read and the output written.  Same arithmetic per target as k_agg.
+constexpr int kFusedMaxLayers = 4;
+constexpr int kFusedMaxHead = 4;
+
+struct FusedLayer {
+  int n_tgt, n_terms, act, f_in_pad, f_out, f_out_pad, K, w_ld, lds_w;
+  const int32_t* tgt_prev;
+  const int32_t* tgt_f0;
+  const int32_t* agg_ptr;
+  const int32_t* agg_src;
+  const int32_t* agg_f0;
+  const int32_t* self_mult;
+  const float* weight;
+  const float* bias;
+  int kind[XPG_MAX_TERMS], rel[XPG_MAX_TERMS], lds_tab[XPG_MAX_TERMS];
+  const float* table[XPG_MAX_TERMS];
+};
+
+struct FusedHead {
+  int k_pad, n_real, n_pad, act;
+  const float* weight;
+  const float* bias;
+};
+
+struct FusedArgs {
+  int64_t rows;
+  const uint32_t* bits;
+  float* y;
+  int words, n0, n_rel, n_layers, n_head, out_col, n_last;
+  const int32_t* f0_node;
+  const int32_t* deg_ptr;
+  const int32_t* deg_src;
+  int shared_floats, wave_floats, o_kin, o_h0, o_h1, o_a;
+  FusedLayer L[kFusedMaxLayers];
+  FusedHead H[kFusedMaxHead];
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ void add4(float4& a, const float4 b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
+template <int WPB>
+__global__ __launch_bounds__(WPB * 64) void k_fused_forward(const FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float fl[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {  // prologue: layer-1 tables and the weights of layers >= 2 into LDS
+    const FusedLayer& L0 = a.L[0];
+    const int n4 = a.n0 * L0.f_out_pad / 4;
+    for (int k = 0; k < L0.n_terms; ++k) {
+      const float4* src = reinterpret_cast<const float4*>(L0.table[k]);
+      float4* dst = reinterpret_cast<float4*>(fl + L0.lds_tab[k]);
+      for (int i = tid; i < n4; i += WPB * 64) dst[i] = src[i];
+    }
+    for (int l = 1; l < a.n_layers; ++l) {
+      const FusedLayer& L = a.L[l];
+      const int k4 = L.K / 4;
+      for (int i = tid; i < L.f_out_pad * k4; i += WPB * 64) {
+        const int o = i / k4, c = i - o * k4;
+        reinterpret_cast<float4*>(fl + L.lds_w + o * L.w_ld)[c] =
+            reinterpret_cast<const float4*>(L.weight + (int64_t)o * L.K)[c];
+      }
+    }
+  }
+  __syncthreads();
+  float* wv = fl + a.shared_floats + wave * a.wave_floats;
+  uint32_t* mb = reinterpret_cast<uint32_t*>(wv);
+  float* kin = wv + a.o_kin;
+  float* Ab = wv + a.o_a;
+
+  for (int64_t row = (int64_t)blockIdx.x * WPB + wave; row < a.rows; row += (int64_t)gridDim.x * WPB) {
+    const uint32_t* rb = a.bits + row * a.words;
+    for (int w = lane; w < a.words; w += 64) mb[w] = rb[w];
+    wave_sync();
+    // kept in-degree per (relation, F_0 node), -1 when the node is masked out
+    for (int idx = lane; idx < a.n_rel * a.n0; idx += 64) {
+      const int r = idx / a.n0, p = idx - r * a.n0;
+      float out = -1.f;
+      if (bit_of(mb, a.f0_node[p])) {
+        const int32_t* pp = a.deg_ptr + r * (a.n0 + 1);
+        const int e0 = pp[p], e1 = pp[p + 1];
+        int c = 0;
+        for (int e = e0; e < e1; ++e) c += bit_of(mb, a.deg_src[e]);
+        out = static_cast<float>(c);
+      }
+      kin[idx] = out;
+    }
+    wave_sync();
+    float* hcur = wv + a.o_h0;
+    float* hprev = wv + a.o_h1;
+    for (int l = 0; l < a.n_layers; ++l) {
+      const FusedLayer& L = a.L[l];
+      const bool l1 = l == 0;
+      const int width = l1 ? L.f_out_pad : L.f_in_pad;
+      const int CH = width >> 2, TPP = 64 / CH;
+      for (int t0 = 0; t0 < L.n_tgt; t0 += TPP) {
+        const int tt = lane / CH, ch = lane - tt * CH, t = t0 + tt;
+        if (tt < TPP && t < L.n_tgt) {
+          const int tf0 = L.tgt_f0[t], tp = L.tgt_prev[t];
+          float4 tot = f4zero();
+          for (int k = 0; k < L.n_terms; ++k) {
+            const int kind = L.kind[k], r = L.rel[k];
+            const float* base = l1 ? fl + L.lds_tab[k] : hprev;
+            const float4 selfv = reinterpret_cast<const float4*>(base + (l1 ? tf0 : tp) * width)[ch];
+            float4 s = f4zero();
+            if (kind == XPG_TERM_ROOT) {
+              s = selfv;
+            } else {
+              const float* kr = kin + r * a.n0;
+              const float kt = kr[tf0];
+              const int32_t* pp = L.agg_ptr + r * (L.n_tgt + 1);
+              const int e0 = pp[t], e1 = pp[t + 1];
+              if (kind == XPG_TERM_GCN) {
+                const float dt = inv_sqrt_deg(kt);
+                fma4(s, dt * dt, selfv);
+                if (kt >= 0.f) {
+                  for (int e = e0; e < e1; ++e) {
+                    const int u0 = L.agg_f0[e];
+                    const float ku = kr[u0];
+                    if (ku >= 0.f) {
+                      const int up = l1 ? u0 : L.agg_src[e];
+                      fma4(s, inv_sqrt_deg(ku) * dt, reinterpret_cast<const float4*>(base + up * width)[ch]);
+                    }
+                  }
+                }
+              } else {  // MEAN
+                if (kt >= 0.f) {
+                  const int sm = L.self_mult[r * L.n_tgt + t];
+                  fma4(s, static_cast<float>(sm), selfv);
+                  for (int e = e0; e < e1; ++e) {
+                    const int u0 = L.agg_f0[e];
+                    if (kr[u0] >= 0.f) add4(s, reinterpret_cast<const float4*>(base + (l1 ? u0 : L.agg_src[e]) * width)[ch]);
+                  }
+                  const float cnt = kt + static_cast<float>(sm);
+                  const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
+                  s.x *= inv; s.y *= inv; s.z *= inv; s.w *= inv;
+                }
+              }
+            }
+            if (l1) add4(tot, s);
+            else reinterpret_cast<float4*>(Ab + tt * L.K + k * width)[ch] = s;
+          }
+          if (l1) {
+            const int f = ch * 4;
+            float v[4] = {tot.x, tot.y, tot.z, tot.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = (f + q < L.f_out) ? act_apply(v[q] + L.bias[f + q], L.act) : 0.f;
+            reinterpret_cast<float4*>(hcur + t * L.f_out_pad)[ch] = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        }
+        if (!l1) {  // dense: h[t][o] = act(sum_k A[t][k] W[o][k] + b[o]) for this pass's targets
+          wave_sync();
+          const float* W = fl + L.lds_w;
+          const int nq = min(TPP, L.n_tgt - t0);
+          for (int o = lane; o < L.f_out_pad; o += 64) {
+            const float bo = o < L.f_out ? L.bias[o] : 0.f;
+            const float4* wr = reinterpret_cast<const float4*>(W + o * L.w_ld);
+            for (int q = 0; q < nq; ++q) {
+              const float4* ar = reinterpret_cast<const float4*>(Ab + q * L.K);
+              float acc = 0.f;
+              for (int k = 0; k < L.K / 4; ++k) {
+                const float4 x = ar[k], wq = wr[k];
+                acc = fmaf(x.x, wq.x, acc);
+                acc = fmaf(x.y, wq.y, acc);
+                acc = fmaf(x.z, wq.z, acc);
+                acc = fmaf(x.w, wq.w, acc);
+              }
+              hcur[(t0 + q) * L.f_out_pad + o] = o < L.f_out ? act_apply(acc + bo, L.act) : 0.f;
+            }
+          }
+        }
+        wave_sync();
+      }
+      float* tmp = hcur;
+      hcur = hprev;
+      hprev = tmp;
+    }
+    // dense head on the last layer's targets (ping-pong through the free H buffer)
+    const float* cur = hprev;
+    int cur_w = a.L[a.n_layers - 1].f_out_pad;
+    float* nxt = hcur;
+    for (int i = 0; i < a.n_head; ++i) {
+      const FusedHead& hd = a.H[i];
+      for (int o = lane; o < hd.n_pad; o += 64) {
+        const float bo = o < hd.n_real ? hd.bias[o] : 0.f;
+        const float4* wr = reinterpret_cast<const float4*>(hd.weight + (int64_t)o * hd.k_pad);
+        for (int t = 0; t < a.n_last; ++t) {
+          const float4* ar = reinterpret_cast<const float4*>(cur + t * cur_w);
+          float acc = 0.f;
+          if (o < hd.n_real) {
+            for (int k = 0; k < hd.k_pad / 4; ++k) {
+              const float4 x = ar[k], wq = wr[k];
+              acc = fmaf(x.x, wq.x, acc);
+              acc = fmaf(x.y, wq.y, acc);
+              acc = fmaf(x.z, wq.z, acc);
+              acc = fmaf(x.w, wq.w, acc);
+            }
+          }
+          nxt[t * hd.n_pad + o] = o < hd.n_real ? act_apply(acc + bo, hd.act) : 0.f;
+        }
+      }
+      wave_sync();
+      float* tmp = const_cast<float*>(cur);
+      cur = nxt;
+      nxt = tmp;
+      cur_w = hd.n_pad;
+    }
+    for (int t = lane; t < a.n_last; t += 64) a.y[row * a.n_last + t] = cur[t * cur_w + a.out_col];
+    wave_sync();
+  }
+}
+
 // ------------------------------------------------------------------------------------ surrogate
 // train_model (wlm.py:132-278) in three stages:
 //  1. k_wlm_stats  (grid, block per Adam step): per-step constants that do not depend on w —
@@ -552,7 +777,7 @@ __device__ uint64_t g_wlm_stamps[2][8];
 #endif
 
 constexpr int kTabPitch = 17;  // 16 entries + 1 pad (bank spread across tables)
-constexpr int kStage = 12;     // staged words per thread per buffer (buffer <= 12K words)
+constexpr int kStage = 10;     // staged words per thread per buffer (buffer <= 10K words)
 
 // In-wave rebuild of the w nibble tables: the 4 columns of table g are owned by 4 adjacent
 // lanes (column i = tid + 1024 c), so each lane shuffles its group's 4 weights and writes 4 of
@@ -588,18 +813,31 @@ __device__ __forceinline__ float nib8(const float* tab, uint32_t word) {
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
-// STAGE: the step's mask rows ([B][words], pitch rp) and column bit vectors ([cols][bw], pitch
-// cp) live in LDS; the next step's copies are loaded into registers right after a barrier and
-// written to LDS just before the next one, so their global latency hides behind a phase.
+// One Adam step = four phases between four workgroup barriers.  Work is cut into WAVE items
+// (64 rows or 64 columns x a slice of words) so that the 32 lanes of an LDS lane group always
+// look up the SAME 16-entry nibble table at distinct rows/columns: every lookup is
+// bank-conflict free, and the slices balance the work over the 16 waves.
+//   B  item (64-row block, word slice): partial p_j over the slice -> bpart[slice][j]
+//   -- barrier A --
+//   G  entry (4-row group, nibble value): p_j = sum of partials, g_j, G tables, p_hist;
+//      Cb(t) stored
+//   -- barrier 1 --
+//   D  item (64-column block, slice of the column bit vectors): partial (M_b^T g)_i -> dpart
+//   -- barrier D --
+//   Adam on owned columns (sum of partials), T rebuilt in-wave, Rb(t+1) / kbuf(t+1) stored
+//   -- barrier 2 --
+// STAGE: the step's mask rows ([batch][rp]), column bit vectors ([cols][cp]) and kernel weights
+// live in LDS; the next copies are loaded into registers right after a barrier and written to
+// LDS just before a later one, so their global latency hides behind a phase.
 template <int CPT, bool STAGE>
 __global__ __launch_bounds__(1024) void k_wlm_fit(
     const uint32_t* __restrict__ bits, const uint32_t* __restrict__ colbits, int64_t rows,
-    int cols, int words, int batch, int bw, const double* __restrict__ kern,
+    int cols, int words, int batch, int bw, int n_bs, int n_ds, const double* __restrict__ kern,
     const WlmStep* __restrict__ stp, xpg_wlm_params P, float* __restrict__ wg,
     float* __restrict__ mg, float* __restrict__ vg, float* __restrict__ p_hist,
     float* __restrict__ w_hist, float* __restrict__ t_glob) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntab = words * 8;        // one table per nibble of every word
   {  // independent fits: one workgroup each, fit-major arrays
     const int64_t f = blockIdx.x;
@@ -614,22 +852,22 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     vg += f * cols;
     p_hist += f * rows;
     w_hist += f * st_ * cols;
-    if (t_glob) t_glob += f * (int64_t)ntab * 17;
+    if (t_glob) t_glob += f * (int64_t)ntab * kTabPitch;
   }
   const int ngrp_alloc = bw * 8;     // g tables cover every nibble of a column word
-  const int ngrp = (batch + 3) / 4;
   const int rp = words | 1, cp = bw | 1;
-  float* G = reinterpret_cast<float*>(smem);                         // [ngrp_alloc][17]
-  float* T = STAGE ? (G + ngrp_alloc * kTabPitch) : t_glob;          // [ntab][17]
-  uint32_t* Rb = reinterpret_cast<uint32_t*>(T + ntab * kTabPitch);  // STAGE: [batch][rp]
-  uint32_t* Cb = Rb + batch * rp;                                     // STAGE: [cols][cp]
+  const int cpad = (cols + 63) & ~63;
+  float* G = reinterpret_cast<float*>(smem);                          // [ngrp_alloc][17]
+  float* bpart = G + ngrp_alloc * kTabPitch;                           // [n_bs][batch]
+  float* dpart = bpart + n_bs * batch;                                 // [n_ds][cpad]
+  const int kb_off = (ngrp_alloc * kTabPitch + n_bs * batch + n_ds * cpad + 1) & ~1;  // 8-B aligned
+  double* kbuf = reinterpret_cast<double*>(G + kb_off);                // STAGE: [batch]
+  float* T = STAGE ? reinterpret_cast<float*>(kbuf + batch) : t_glob;  // [ntab][17]
+  uint32_t* Rb = reinterpret_cast<uint32_t*>(T + ntab * kTabPitch);   // STAGE: [batch][rp]
+  uint32_t* Cb = Rb + batch * rp;                                      // STAGE: [cols][cp]
 
-  // prediction layout: tpr lanes per mask row (power of 2, <= 16 so a wave holds >= 4 rows)
-  int cap = batch < 1024 ? batch : 1024;
-  int tpr = 16;
-  while (tpr > 1 && 1024 / tpr < cap) tpr >>= 1;
-  const int rpp = 1024 / tpr, rows_w = 64 / tpr, sub = tid & (tpr - 1);
-  const int passes = (batch + rpp - 1) / rpp;
+  const int nrb = (batch + 63) >> 6, ncb = (cols + 63) >> 6;
+  const int bsw = (words + n_bs - 1) / n_bs, dsw = (bw + n_ds - 1) / n_ds;
   const float l1s = P.l1_lambda / static_cast<float>(cols);
   const int64_t nsteps = (rows + batch - 1) / batch;
 
@@ -645,6 +883,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
   wlm_build_T<CPT>(w, T, ntab);
 
   uint32_t stg[kStage];
+  double kst = 0.0;
   // stage-load helpers (flat element index q*1024 + tid over the buffer's logical extent)
 #define XPG_ROWS_LOAD(TT)                                                               \
   {                                                                                     \
@@ -657,13 +896,19 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       const uint32_t x_ = src_[e_ < n_ ? e_ : n_ - 1];                                  \
       stg[q] = e_ < n_ ? x_ : 0u;                                                       \
     }                                                                                   \
+    const double k_ = kern[r0_ + (tid < B_ ? tid : B_ - 1)];                            \
+    kst = tid < B_ ? k_ : 0.0;                                                          \
   }
-#define XPG_ROWS_STORE()                                                                \
+#define XPG_ROWS_STORE(TT)                                                              \
   {                                                                                     \
     _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
       const int e_ = q * 1024 + tid;                                                    \
       if (e_ < batch * words) Rb[(e_ / words) * rp + (e_ % words)] = stg[q];            \
     }                                                                                   \
+    const int64_t r0_ = (TT) * batch;                                                   \
+    const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);      \
+    if (tid < batch) kbuf[tid] = kst;                                                   \
+    for (int e_ = tid + 1024; e_ < B_; e_ += 1024) kbuf[e_] = kern[r0_ + e_];           \
   }
 #define XPG_COLS_LOAD(TT)                                                               \
   {                                                                                     \
@@ -681,12 +926,12 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       if (e_ < cols * bw) Cb[(e_ / bw) * cp + (e_ % bw)] = stg[q];                      \
     }                                                                                   \
   }
-  // schedule: Cb(t) is loaded at the start of phase B(t) and stored before barrier 1 (the
-  // previous reader, D(t-1), finished at barrier 2); Rb(t+1) is loaded at the start of D(t)
-  // and stored before barrier 2 (its previous reader, B(t), finished at barrier 1).
+  // schedule: Cb(t) is loaded at the start of phase B(t) and stored before barrier 1 (its
+  // previous reader, D(t-1), finished at barrier D); Rb(t+1) and kbuf(t+1) are loaded after
+  // barrier 1 and stored before barrier 2 (their readers, B(t) and G(t), finished at barrier 1).
   if (STAGE) {
     XPG_ROWS_LOAD(0)
-    XPG_ROWS_STORE()
+    XPG_ROWS_STORE(0)
   }
   __syncthreads();
 #ifdef XPG_WLM_STAMPS
@@ -704,82 +949,97 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       const int i = tid + c * 1024;
       if (i < cols) w_hist[t * cols + i] = w[c];
     }
-    // ---- predictions p_j = M_b[j] . w and g_j; nibble tables of g built inside each wave
-    for (int ps = 0; ps < passes; ++ps) {
-      const int j = ps * rpp + tid / tpr;
+    // ---- B: partial predictions p_j = M_b[j] . w over a slice of words (lanes = rows)
+    for (int it = wave; it < nrb * n_bs; it += 16) {
+      const int rb = it % nrb, sl = it / nrb;
+      const int j = rb * 64 + lane;
+      const int wd0 = sl * bsw, wd1 = min(words, wd0 + bsw);
       float s = 0.f;
       if (j < B) {
-        if (STAGE) {
-          const uint32_t* row = Rb + j * rp;
-          for (int k0 = 0; k0 * tpr < words; k0 += 4) {
-            uint32_t wv[4];
+        const uint32_t* row = STAGE ? (Rb + j * rp) : (bits + (r0 + j) * words);
+        for (int k0 = wd0; k0 < wd1; k0 += 2) {  // 16 lookups in flight (lgkmcnt limit 15)
+          uint32_t wv[2];
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const int wd = sub + (k0 + h) * tpr;
-              wv[h] = row[wd < words ? wd : 0];
-            }
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const int wd = sub + (k0 + h) * tpr;
-              const float x = nib8(T + ((wd < words ? wd : 0) * 8) * kTabPitch, wv[h]);
-              s += wd < words ? x : 0.f;
-            }
+          for (int h = 0; h < 2; ++h) {
+            const int wd = k0 + h;
+            wv[h] = row[wd < wd1 ? wd : wd0];
           }
-        } else {
-          const uint32_t* row = bits + (r0 + j) * words;
-#pragma unroll 2
-          for (int wd = sub; wd < words; wd += tpr) s += nib8(T + (wd * 8) * kTabPitch, row[wd]);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int wd = k0 + h;
+            const float x = nib8(T + ((wd < wd1 ? wd : wd0) * 8) * kTabPitch, wv[h]);
+            s += wd < wd1 ? x : 0.f;
+          }
         }
       }
-      XPG_STAMP(0)
-      for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      float g = 0.f;
-      if (j < B) {
-        if (sub == 0) p_hist[r0 + j] = s;
-        const double kj = kern[r0 + j];
-        g = static_cast<float>(2.0 * kj * (static_cast<double>(s) - sc.ybar) /
-                               (static_cast<double>(B) * sc.ksum));
-      }
-      const int jw0 = ps * rpp + (tid >> 6) * rows_w;  // first batch row held by this wave
-      const int ent_w = rows_w * 4;                    // 16 entries per 4-row group
-      for (int e0 = 0; e0 < ent_w; e0 += 64) {
-        const int e = e0 + lane;
-        const int gl = e >> 4, vv = e & 15;
+      if (j < batch) bpart[sl * batch + j] = s;
+    }
+    XPG_STAMP(0)
+    __syncthreads();  // bpart complete
+    XPG_STAMP(1)
+    // ---- G: g_j = 2 k_j (p_j - ybar) / (B sum k) and the nibble tables of g over 4-row groups
+    {
+      const int ngrp = (B + 3) >> 2;
+      const double cg = 2.0 / (static_cast<double>(B) * sc.ksum);
+      for (int e = tid; e < ngrp * 16; e += 1024) {
+        const int grp = e >> 4, vv = e & 15;
         float acc = 0.f;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          int src = 4 * gl + b;
-          src = src < rows_w ? src : rows_w - 1;
-          const float gb = __shfl(g, src * tpr, 64);
-          acc += ((vv >> b) & 1) ? gb : 0.f;
+          const int j = 4 * grp + b;
+          float g = 0.f;
+          if (j < B) {
+            float p = 0.f;
+            for (int sl = 0; sl < n_bs; ++sl) p += bpart[sl * batch + j];
+            const double kj = STAGE ? kbuf[j] : kern[r0 + j];
+            g = static_cast<float>(kj * cg * (static_cast<double>(p) - sc.ybar));
+            if (vv == b) p_hist[r0 + j] = p;
+          }
+          acc += ((vv >> b) & 1) ? g : 0.f;
         }
-        const int grp = (jw0 >> 2) + gl;
-        if (e < ent_w && grp < ngrp) G[grp * kTabPitch + vv] = acc;
+        G[grp * kTabPitch + vv] = acc;
       }
     }
-    XPG_STAMP(1)
     if (STAGE) XPG_COLS_STORE()
     XPG_STAMP(2)
-    __syncthreads();  // G and Cb(t) complete; Rb free
+    __syncthreads();  // G and Cb(t) complete; Rb, kbuf free
     XPG_STAMP(3)
     if (STAGE && t + 1 < nsteps) XPG_ROWS_LOAD(t + 1)
-    // ---- gradient M_b^T g + L1 subgradient + L2 decay; Adam (torch single-tensor order)
+    // ---- D: partial gradient (M_b^T g)_i over a slice of the column's row words (lanes = columns)
+    for (int it = wave; it < ncb * n_ds; it += 16) {
+      const int cbk = it % ncb, sl = it / ncb;
+      const int i = cbk * 64 + lane;
+      const int k0 = sl * dsw, k1 = min(bw, k0 + dsw);
+      float s = 0.f;
+      if (i < cols) {
+        const uint32_t* cb = STAGE ? (Cb + i * cp) : (colbits + (t * cols + i) * bw);
+        for (int kk = k0; kk < k1; kk += 2) {
+          uint32_t wv[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = kk + h;
+            wv[h] = cb[k < k1 ? k : k0];
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = kk + h;
+            const float x = nib8(G + ((k < k1 ? k : k0) * 8) * kTabPitch, wv[h]);
+            s += k < k1 ? x : 0.f;
+          }
+        }
+      }
+      dpart[sl * cpad + i] = s;
+    }
+    XPG_STAMP(4)
+    __syncthreads();  // dpart complete
+    XPG_STAMP(5)
+    // ---- L1 subgradient + L2 decay; Adam (torch single-tensor order) on the owned columns
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int i = tid + c * 1024;
       if (i < cols) {
         float s = 0.f;
-        const uint32_t* cb = STAGE ? (Cb + i * cp) : (colbits + (t * cols + i) * bw);
-        for (int k0 = 0; k0 < bw; k0 += 4) {
-          uint32_t wv[4];
-#pragma unroll
-          for (int h = 0; h < 4; ++h) wv[h] = cb[k0 + h < bw ? k0 + h : 0];
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const float x = nib8(G + ((k0 + h < bw ? k0 + h : 0) * 8) * kTabPitch, wv[h]);
-            s += k0 + h < bw ? x : 0.f;
-          }
-        }
+        for (int sl = 0; sl < n_ds; ++sl) s += dpart[sl * cpad + i];
         const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
         float g = fmaf(l1s, sg, s);
         g = fmaf(P.weight_decay, w[c], g);
@@ -789,10 +1049,8 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
         w[c] = w[c] - sc.step_size * (m[c] / denom);
       }
     }
-    XPG_STAMP(4)
     wlm_build_T<CPT>(w, T, ntab);
-    XPG_STAMP(5)
-    if (STAGE && t + 1 < nsteps) XPG_ROWS_STORE()
+    if (STAGE && t + 1 < nsteps) XPG_ROWS_STORE(t + 1)
     XPG_STAMP(6)
     __syncthreads();
     XPG_STAMP(7)
@@ -946,6 +1204,114 @@ int launch_agg(const AggArgs& a, hipStream_t st) {
   return fail(XPG_EINVAL, "agg: unsupported row width " + std::to_string(a.width));
 }
 
+// Fused single-launch forward when the plan fits (returns 1 when it does not apply).
+int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
+  const char* env = getenv("XPG_FORWARD");
+  if (env && std::strcmp(env, "unfused") == 0) return 1;
+  if (p->n_layers > kFusedMaxLayers || p->n_head > kFusedMaxHead) return 1;
+  FusedArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.rows = rows;
+  a.bits = bits;
+  a.y = y;
+  a.words = words_of(p->cols);
+  a.n0 = p->n0;
+  a.n_rel = p->n_rel;
+  a.n_layers = p->n_layers;
+  a.n_head = p->n_head;
+  a.out_col = p->out_col;
+  a.n_last = p->layers[p->n_layers - 1].n_tgt;
+  a.f0_node = p->f0_node;
+  a.deg_ptr = p->deg_ptr;
+  a.deg_src = p->deg_src;
+  auto up4 = [](int64_t x) { return (x + 3) & ~int64_t(3); };
+  int64_t shared = 0, h_max = 0, a_max = 0;
+  for (int l = 0; l < p->n_layers; ++l) {
+    const xpg_layer_desc& ly = p->layers[l];
+    FusedLayer& L = a.L[l];
+    if (ly.f_out_pad > 256 || ly.f_out_pad % 32 || ly.n_terms < 1 || ly.n_terms > XPG_MAX_TERMS) return 1;
+    L.n_tgt = ly.n_tgt;
+    L.n_terms = ly.n_terms;
+    L.act = ly.act;
+    L.f_in_pad = ly.f_in_pad;
+    L.f_out = ly.f_out;
+    L.f_out_pad = ly.f_out_pad;
+    L.tgt_prev = ly.tgt_prev;
+    L.tgt_f0 = ly.tgt_f0;
+    L.agg_ptr = ly.agg_ptr;
+    L.agg_src = ly.agg_src;
+    L.agg_f0 = ly.agg_f0;
+    L.self_mult = ly.self_mult;
+    L.weight = ly.weight;
+    L.bias = ly.bias;
+    for (int k = 0; k < ly.n_terms; ++k) {
+      L.kind[k] = ly.terms[k].kind;
+      L.rel[k] = ly.terms[k].rel;
+      L.table[k] = ly.terms[k].table;
+    }
+    h_max = std::max<int64_t>(h_max, (int64_t)ly.n_tgt * ly.f_out_pad);
+    if (l == 0) {
+      for (int k = 0; k < ly.n_terms; ++k) {
+        if (!ly.terms[k].table) return 1;
+        L.lds_tab[k] = static_cast<int>(shared);
+        shared += up4((int64_t)p->n0 * ly.f_out_pad);
+      }
+    } else {
+      const xpg_layer_desc& prev = p->layers[l - 1];
+      if (ly.f_in_pad != prev.f_out_pad || !ly.weight) return 1;
+      L.K = ly.n_terms * ly.f_in_pad;
+      L.w_ld = L.K + 4;  // 16-B rows, bank-shifted by 4 words per output row
+      L.lds_w = static_cast<int>(shared);
+      shared += (int64_t)ly.f_out_pad * L.w_ld;
+      const int tpp = 64 / (ly.f_in_pad / 4);
+      a_max = std::max<int64_t>(a_max, (int64_t)tpp * L.K);
+    }
+  }
+  int cur_w = p->layers[p->n_layers - 1].f_out_pad;
+  for (int i = 0; i < p->n_head; ++i) {
+    const xpg_head_desc& hd = p->head[i];
+    if (hd.k_pad != cur_w || hd.k_pad % 4) return 1;
+    a.H[i].k_pad = hd.k_pad;
+    a.H[i].n_real = hd.n_real;
+    a.H[i].n_pad = hd.n_pad;
+    a.H[i].act = hd.act;
+    a.H[i].weight = hd.weight;
+    a.H[i].bias = hd.bias;
+    h_max = std::max<int64_t>(h_max, (int64_t)a.n_last * hd.n_pad);
+    cur_w = hd.n_pad;
+  }
+  if (p->out_col < 0 || p->out_col >= cur_w) return 1;
+  a.shared_floats = static_cast<int>(shared);
+  a.o_kin = static_cast<int>(up4(a.words));
+  a.o_h0 = a.o_kin + static_cast<int>(up4((int64_t)p->n_rel * p->n0));
+  a.o_h1 = a.o_h0 + static_cast<int>(up4(h_max));
+  a.o_a = a.o_h1 + static_cast<int>(up4(h_max));
+  a.wave_floats = a.o_a + static_cast<int>(up4(a_max));
+  const int64_t lds_cap = 160 * 1024 / 4 - 64;
+  int wpb = 0;
+  for (int c : {8, 4, 2}) {
+    if (shared + (int64_t)c * a.wave_floats <= lds_cap) {
+      wpb = c;
+      break;
+    }
+  }
+  if (!wpb) return 1;
+  const size_t lds = sizeof(float) * (size_t)(shared + (int64_t)wpb * a.wave_floats);
+  const int64_t per_cu = std::max<int64_t>(1, (160 * 1024) / (int64_t)lds);
+  const int64_t grid = std::min<int64_t>(cdiv(rows, wpb), 256 * per_cu);
+#define XPG_FUSED(W)                                                                                     \
+  if (wpb == W) {                                                                                        \
+    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_forward<W>),                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));       \
+    hipLaunchKernelGGL(k_fused_forward<W>, dim3(static_cast<unsigned>(grid)), dim3(W * 64), lds, st, a); \
+    XPG_LAUNCHED();                                                                                      \
+    return XPG_OK;                                                                                       \
+  }
+  XPG_FUSED(8) XPG_FUSED(4) XPG_FUSED(2)
+#undef XPG_FUSED
+  return 1;
+}
+
 }  // namespace
 
 // ==================================================================================== C-ABI
@@ -1040,6 +1406,8 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   XPG_REQ(p->n_rel >= 1 && p->n0 >= 1 && p->cols > 0, "masked_forward: bad plan sizes");
   if (rows == 0) return XPG_OK;
   hipStream_t st = S(stream);
+  rc = try_fused_forward(p, bits, rows, y, st);
+  if (rc != 1) return rc;
   char* ws = static_cast<char*>(workspace);
   float* kin = reinterpret_cast<float*>(ws + L.kin);
   const int words = words_of(p->cols);
@@ -1120,10 +1488,25 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
 
 struct WlmWs {
   size_t steps_off, colbits_off, phist_off, whist_off, tglob_off, total;
-  int bw;
+  int bw, n_bs, n_ds;
   bool stage;
   size_t lds;
 };
+
+// Word slices per wave item: minimise (rounds of 16 waves) x (words per item + 1 for the item's
+// fixed cost) over blocks x slices items.
+static int wlm_slices(int64_t blocks, int words) {
+  int best = 1;
+  int64_t best_cost = INT64_MAX;
+  for (int n = 1; n <= words; ++n) {
+    const int64_t cost = cdiv(blocks * n, 16) * (cdiv(words, n) + 1);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = n;
+    }
+  }
+  return best;
+}
 
 static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
   XPG_REQ(n_fits > 0 && rows > 0 && cols > 0 && batch > 0, "wlm_fit: bad arguments");
@@ -1132,14 +1515,24 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   const int64_t steps = cdiv(rows, batch);
   const int words = words_of(cols);
   L->bw = static_cast<int>(cdiv(batch, 32));
-  const size_t g_bytes = sizeof(float) * (size_t)(L->bw * 8 * kTabPitch);
-  const size_t t_bytes = sizeof(float) * (size_t)words * 8 * kTabPitch;
-  const size_t stage_bytes = sizeof(uint32_t) * ((size_t)batch * (words | 1) + (size_t)cols * (L->bw | 1));
+  L->n_bs = wlm_slices(cdiv(batch, 64), words);
+  L->n_ds = wlm_slices(cdiv(cols, 64), L->bw);
+  const int64_t cpad = (cols + 63) & ~int64_t(63);
   const size_t lds_cap = 150 * 1024;
-  XPG_REQ(g_bytes <= lds_cap, "wlm_fit: batch too large for the single-workgroup fit (LDS)");
-  L->stage = g_bytes + t_bytes + stage_bytes <= lds_cap && (int64_t)batch * words <= kStage * 1024 &&
+  auto g_bytes = [&]() {  // G tables + partial sums, rounded to 8 B (the kernel's kb_off)
+    return sizeof(float) * (size_t)((L->bw * 8 * kTabPitch + L->n_bs * batch + L->n_ds * cpad + 1) & ~int64_t(1));
+  };
+  while (g_bytes() > lds_cap && (L->n_bs > 1 || L->n_ds > 1)) {
+    if (L->n_ds > 1) L->n_ds = 1;
+    else L->n_bs = 1;
+  }
+  XPG_REQ(g_bytes() <= lds_cap, "wlm_fit: batch too large for the single-workgroup fit (LDS)");
+  const size_t t_bytes = sizeof(float) * (size_t)words * 8 * kTabPitch;
+  const size_t stage_bytes = sizeof(double) * (size_t)batch +
+                             sizeof(uint32_t) * ((size_t)batch * (words | 1) + (size_t)cols * (L->bw | 1));
+  L->stage = g_bytes() + t_bytes + stage_bytes <= lds_cap && (int64_t)batch * words <= kStage * 1024 &&
              cols * (int64_t)L->bw <= kStage * 1024;
-  L->lds = g_bytes + (L->stage ? t_bytes + stage_bytes : 0);
+  L->lds = g_bytes() + (L->stage ? t_bytes + stage_bytes : 0);
   const size_t F = static_cast<size_t>(n_fits);
   size_t off = 0;
   L->steps_off = off;
@@ -1198,7 +1591,8 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
     XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit<C, TL>),                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds)));     \
     hipLaunchKernelGGL((k_wlm_fit<C, TL>), dim3(nf), dim3(1024), L.lds, st, bits, colbits, rows, ic, words, \
-                       ib, L.bw, kernel, stp, *params, w, adam_m, adam_v, p_hist, w_hist, t_glob);         \
+                       ib, L.bw, L.n_bs, L.n_ds, kernel, stp, *params, w, adam_m, adam_v, p_hist, w_hist,  \
+                       t_glob);                                                                            \
     XPG_LAUNCHED();                                                                                        \
     goto fitted;                                                                                           \
   }

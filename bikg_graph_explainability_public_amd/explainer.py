@@ -16,7 +16,7 @@ import warnings
 import numpy as np
 import torch
 
-from . import _lib, engine, pipeline
+from . import _lib, engine, pipeline, sharding
 from .data import Data
 from .masks import Mask, dataloader_seed_draw
 from .model import Model
@@ -54,6 +54,7 @@ class Explainer:
         self.node_types = node_types
         self.edge_types = edge_types
         self.last_run = None  # diagnostics of the last run (per-repeat losses, path used)
+        self.group = None     # torch.distributed process group for multi-GPU runs (None = world)
 
     @staticmethod
     def initial_assertions(feat, edge_index, arch, params, names, pathways, pathway_names,
@@ -218,18 +219,44 @@ class Explainer:
         R = bits_list[0].shape[0]
         batch = R // epochs
         bits = torch.stack(bits_list)                       # [times, R, W]
+        # multi-GPU (torch.distributed initialised, one process per GPU): rows of the forward /
+        # KernelSHAP and whole surrogate fits are sharded over ranks, outputs all-gathered, so
+        # every rank returns the single-GPU result (sharding.py).
+        flat = bits.reshape(times * R, -1)
+        g = self.group
         if plan is not None:
-            y = plan.forward(bits.reshape(times * R, -1))[:, 0].reshape(times, R)
+            y = sharding.gather_map(times * R, lambda s, e: plan.forward(flat[s:e])[:, 0],
+                                    g).reshape(times, R)
         else:
-            ys = []
-            for b_, m_ in zip(bits_list, masks):
-                m_ = engine.unpack_masks(b_, S) if m_ is None else m_
-                ys.append(pipeline.generic_outputs(self.arch, sub_feat, sub_ei, m_, sub_ind,
-                                                   self.problem, *geo, batch=batch))
-            y = torch.stack(ys)
-        kern = engine.shap_kernel(bits.reshape(times * R, -1), S).reshape(times, R)
-        w, losses, best, _, _ = engine.wlm_fit(bits, S, batch, y, kern,
-                                               torch.stack(w0_list), self.params)
+            def generic(t0, t1):
+                ys = [pipeline.generic_outputs(
+                    self.arch, sub_feat, sub_ei,
+                    engine.unpack_masks(bits_list[i], S) if masks[i] is None else masks[i],
+                    sub_ind, self.problem, *geo, batch=batch) for i in range(t0, t1)]
+                return torch.stack(ys) if ys else torch.empty((0, R), device=device)
+            y = sharding.gather_map(times, generic, g)
+
+        def kernel_rows(s, e):
+            if e == s:
+                return torch.empty(0, dtype=torch.float64, device=device)
+            return engine.shap_kernel(flat[s:e], S)
+        kern = sharding.gather_map(times * R, kernel_rows, g).reshape(times, R)
+
+        fits = {}
+
+        def fit(t0, t1):
+            if t1 == t0:
+                n_steps = -(-R // batch)
+                fits["losses"] = torch.empty((0, n_steps), dtype=torch.float64, device=device)
+                fits["best"] = torch.empty(0, dtype=torch.int32, device=device)
+                return torch.empty((0, S), device=device)
+            w_, fits["losses"], fits["best"], _, _ = engine.wlm_fit(
+                bits[t0:t1], S, batch, y[t0:t1], kern[t0:t1], torch.stack(w0_list[t0:t1]),
+                self.params)
+            return w_
+        w = sharding.gather_map(times, fit, g)
+        losses = sharding.gather_rows(fits["losses"], times, g)
+        best = sharding.gather_rows(fits["best"], times, g)
         config_vals = [w[i] for i in range(times)]
         diag = [{"losses": losses[i], "best_epoch": best[i], "rows": R, "batch": batch,
                  "y": y[i], "bits": bits[i]} for i in range(times)]

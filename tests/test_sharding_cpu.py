@@ -1,0 +1,119 @@
+"""Multi-process (gloo, CPU) tests of the multi-GPU sharding used by Explainer.run and bench.py
+(bikg_graph_explainability_public_amd/sharding.py).
+
+The per-shard compute here is the numpy oracle (test infrastructure) standing in for the HIP
+engine, so the test checks the orchestration — row shards of the forward / KernelSHAP, repeat
+shards of the surrogate fits, all-gathers in global order — against the reference's own golden
+outputs for the `test_run` fixture (3 repeats), at world sizes 2 and 3."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+from bikg_graph_explainability_public_amd import sharding  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _worker_gather(rank, world, port):
+    _init(rank, world, port)
+    try:
+        for n in (0, 1, world - 1, world, 7, 13):
+            for dt in (torch.float32, torch.float64, torch.int32):
+                full = (torch.arange(n * 3, dtype=torch.float64) * 1.5 - 2).to(dt).reshape(n, 3)
+                s, e = sharding.shard_range(n, world, rank)
+                got = sharding.gather_rows(full[s:e].clone(), n)
+                assert got.dtype == dt and torch.equal(got, full), (n, dt)
+                got = sharding.gather_map(n, lambda a, b: full[a:b] * 1)
+                assert torch.equal(got, full)
+        try:
+            sharding.gather_rows(torch.zeros(world + 5, 2), 4)
+        except ValueError:
+            pass
+        else:
+            raise AssertionError("wrong shard size accepted")
+    finally:
+        dist.destroy_process_group()
+
+
+def _worker_pipeline(rank, world, port):
+    import oracle
+    from golden_utils import repeat_masks
+    from test_oracle_golden import prepare
+    _init(rank, world, port)
+    try:
+        z, meta, spec, sub_x, rel_ei, sub_ind = prepare("test_run")
+        masks = repeat_masks(z, meta)
+        times, (R, S) = len(masks), masks[0].shape
+        flat = np.concatenate(masks, 0)
+        y = sharding.gather_map(times * R, lambda s, e: torch.from_numpy(
+            oracle.masked_query_outputs(spec, sub_x, rel_ei, flat[s:e], sub_ind)
+            if e > s else np.zeros(0))).reshape(times, R)
+        k = sharding.gather_map(times * R, lambda s, e: torch.from_numpy(
+            oracle.shap_kernel(flat[s:e]) if e > s else np.zeros(0))).reshape(times, R)
+        bs = meta["r0_batch_size"]
+
+        def fit(t0, t1):
+            ws = [oracle.train_wlm(masks[i], bs, y[i].numpy(), k[i].numpy(), z[f"r{i}_w0"],
+                                   meta["params"])[0] for i in range(t0, t1)]
+            return torch.from_numpy(np.stack(ws)) if ws else torch.zeros((0, S), dtype=torch.float64)
+        w = sharding.gather_map(times, fit)
+        for i in range(times):
+            np.testing.assert_allclose(y[i].numpy(), z[f"r{i}_output"], rtol=0, atol=2e-6)
+            np.testing.assert_allclose(k[i].numpy(), z[f"r{i}_kernel"], rtol=1e-12, atol=0)
+            np.testing.assert_allclose(w[i].numpy(), z[f"r{i}_w_final"], rtol=0, atol=2e-5)
+        # weight_stacking over the gathered repeats is identical on every rank
+        mean = w.mean(0)
+        ref = torch.empty_like(mean)
+        ref.copy_(mean)
+        dist.broadcast(ref, 0)
+        assert torch.equal(ref, mean)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 5, 12800, 12801):
+        for world in (1, 2, 3, 8):
+            spans = [sharding.shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [e - s for s, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        sharding.shard_range(4, 2, 2)
+
+
+def test_world_info_single_process():
+    assert sharding.world_info() == (1, 0)
+    x = torch.arange(6).reshape(3, 2)
+    assert sharding.gather_rows(x, 3) is x
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_rows_gloo(world):
+    mp.spawn(_worker_gather, args=(world, _free_port()), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pipeline_matches_reference_gloo(world):
+    mp.spawn(_worker_pipeline, args=(world, _free_port()), nprocs=world, join=True)

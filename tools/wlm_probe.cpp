@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     const int64_t steps = (R + batch - 1) / batch;
     printf("S=%ld R=%ld batch=%ld: fit chain %.1f us (%.2f us/step); cycles/step per segment:\n", (long)S, (long)R,
            (long)batch, ms * 1e3, ms * 1e3 / steps);
-    const char* nm[8] = {"B lookups", "B reduce+G", "COLS_STORE", "sync1", "D grad+adam", "T build", "ROWS_STORE", "sync2"};
+    const char* nm[8] = {"B lookups", "syncA", "G + COLS_ST", "sync1", "D lookups", "syncD", "Adam+T+ROWS", "sync2"};
     for (int q = 0; q < 8; ++q) printf("  %-12s wave0 %8.0f  last %8.0f\n", nm[q], (double)st[0][q] / steps, (double)st[1][q] / steps);
   }
   return 0;
