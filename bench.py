@@ -101,6 +101,25 @@ def wlm_bytes(rows, cols, batch):
     return rows * W * 4 + rows * (4 + 8) + cols * 4 * 6 + 8 * math.ceil(rows / batch)
 
 
+def pmc_traffic(kernels, args):
+    """HBM bytes per launch of the dominant launch chain from the committed PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE runs of this bench at its default configuration), or None."""
+    fn = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    default = (args.nodes, args.edges, args.feat, args.interpret_samples, args.epochs,
+               args.repeats) == (100_000, 1_000_000, 64, 256, 50, 1)
+    if not default or not os.path.exists(fn):
+        return None, None
+    data = json.load(open(fn))
+    tot, hit = 0.0, False
+    for name, d in data.items():
+        if name.startswith(kernels) and d.get("traffic_bytes") is not None:
+            tot += d["traffic_bytes"]
+            hit = True
+    return (tot if hit else None), ("profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE, "
+                                    "summed over the chain's kernels)" if hit else None)
+
+
 def cpu_baseline(args, arch, sub_feat, sub_ei, q):
     """The numpy oracle (CPU restatement of the reference path, 1 thread) on a bounded sample
     of the same workload: cpu_rows mask rows through forward + KernelSHAP + surrogate."""
@@ -204,17 +223,22 @@ def main():
         dominant = max(phase_ms, key=phase_ms.get)
         if dominant == "wlm":
             bytes_launch = wlm_bytes(R, S, batch) * T
-            kname = "k_wlm (surrogate Adam loop, 1 persistent workgroup)"
+            kname = "surrogate fit chain (k_wlm_stats, k_wlm_colbits, k_wlm_fit, k_wlm_loss)"
+            kernels = ("k_wlm_stats", "k_wlm_colbits", "k_wlm_fit", "k_wlm_loss", "k_argmin_first")
         elif dominant == "forward":
             bytes_launch = forward_bytes(plan, R * T)
-            kname = "masked forward chain (k_degree + k_agg + k_dense + k_take_col)"
+            kname = "masked forward chain (k_degree, k_agg, k_dense, k_take_col)"
+            kernels = ("k_degree", "k_agg", "k_dense", "k_take_col", "k_fused_forward")
         elif dominant == "shap":
             bytes_launch = T * R * (((S + 31) // 32) * 4 + 12)
             kname = "k_popcount + k_shap"
+            kernels = ("k_popcount", "k_shap")
         else:
             bytes_launch = T * R * ((S + 31) // 32) * 4
             kname = "k_shapley"
+            kernels = ("k_shapley",)
         achieved = bytes_launch / (phase_ms[dominant] * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(kernels, args)
         line = {
             "metric": METRIC,
             "value": total_rows / elapsed,
@@ -241,7 +265,8 @@ def main():
             "phases_ms": phase_ms,
             "roofline": {"kernel": kname, "bound": "hbm", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "bytes_per_launch": bytes_launch},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "bytes_per_launch": bytes_launch},
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, arch, sub_feat, sub_ei, q)

@@ -1075,6 +1075,306 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
 #undef XPG_COLS_STORE
 }
 
+// Multi-workgroup fit (cols large enough to split): P workgroups per fit, one per CU, each
+// owning a contiguous slice of mask words (its columns: w, Adam moments, T tables, column bit
+// vectors).  Per Adam step the partial predictions over each slice are exchanged through memory
+// (MI355X_MICROARCH.md inter-workgroup hand-off: 8-byte {value, step tag} granules, stored and
+// polled with sc1) and summed in a fixed order, so every workgroup derives the same g; the gradient and Adam update of a
+// column stay with its owner.  The poll is bounded: a grid that is not co-resident ends (with
+// an error flag) instead of hanging.
+constexpr uint32_t kMcSpinLimit = 1u << 21;
+
+__device__ __forceinline__ void st64_sc1(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld64_sc1(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int kMcMaxP = 8;
+
+template <int CPT>
+__global__ __launch_bounds__(1024) void k_wlm_fit_mc(
+    const uint32_t* __restrict__ bits, const uint32_t* __restrict__ colbits, int64_t rows, int cols, int words,
+    int batch, int bw, int P, int wpp, int n_bs, int n_ds, int64_t n_fits, int xcd_local,
+    const double* __restrict__ kern,
+    const WlmStep* __restrict__ stp, xpg_wlm_params Pm, float* __restrict__ wg, float* __restrict__ mg,
+    float* __restrict__ vg, float* __restrict__ p_hist, float* __restrict__ w_hist, uint64_t* xp,
+    uint32_t* err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int64_t f;
+  int part;
+  if (xcd_local) {  // blocks b and b + 8 share an XCD (observed round-robin dealing, speed only)
+    const int64_t k = blockIdx.x >> 3, g = k / P;
+    part = static_cast<int>(k - g * P);
+    f = g * 8 + (blockIdx.x & 7);
+    if (f >= n_fits) return;  // filler block (whole workgroup)
+  } else {
+    f = blockIdx.x / P;
+    part = static_cast<int>(blockIdx.x - f * P);
+  }
+  const int64_t nsteps = (rows + batch - 1) / batch;
+  const int w_lo = min(words, part * wpp), w_hi = min(words, w_lo + wpp);
+  const int ow = w_hi - w_lo;                       // own words (0 for surplus parts)
+  const int c_lo = w_lo * 32, ncol = max(0, min(cols, w_hi * 32) - c_lo);
+  bits += f * rows * words;
+  colbits += f * nsteps * cols * bw;
+  kern += f * rows;
+  stp += f * nsteps;
+  wg += f * cols + c_lo;
+  mg += f * cols + c_lo;
+  vg += f * cols + c_lo;
+  p_hist += f * rows;
+  w_hist += f * nsteps * cols + c_lo;
+  xp += f * 2 * P * (int64_t)batch;
+
+  const int ngrp_alloc = bw * 8;
+  const int ow_max = wpp, ncol_max = wpp * 32;
+  const int rp = ow_max | 1, cp = bw | 1;
+  const int cpad = (ncol_max + 63) & ~63;
+  float* G = reinterpret_cast<float*>(smem);                         // [ngrp_alloc][17]
+  float* bpart = G + ngrp_alloc * kTabPitch;                          // [n_bs][batch]
+  float* dpart = bpart + n_bs * batch;                                // [n_ds][cpad]
+  float* pg = dpart + n_ds * cpad;                                    // [batch] g_j
+  float* xv = pg + batch;                                             // [P][batch] partials
+  const int kb_off = (ngrp_alloc * kTabPitch + n_bs * batch + n_ds * cpad + batch + P * batch + 1) & ~1;
+  double* kbuf = reinterpret_cast<double*>(G + kb_off);              // [batch]
+  float* T = reinterpret_cast<float*>(kbuf + batch);                 // [ow_max*8][17]
+  uint32_t* Rb = reinterpret_cast<uint32_t*>(T + ow_max * 8 * kTabPitch);  // [batch][rp]
+  uint32_t* Cb = Rb + batch * rp;                                     // [ncol_max][cp]
+
+  const int nrb = (batch + 63) >> 6, ncb = (ncol + 63) >> 6;
+  const int bsw = (ow + n_bs - 1) / max(n_bs, 1), dsw = (bw + n_ds - 1) / n_ds;
+  const float l1s = Pm.l1_lambda / static_cast<float>(cols);
+
+  float w[CPT], m[CPT], v[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int i = tid + c * 1024;
+    w[c] = i < ncol ? wg[i] : 0.f;
+    m[c] = i < ncol ? mg[i] : 0.f;
+    v[c] = i < ncol ? vg[i] : 0.f;
+  }
+  for (int e = tid; e < ngrp_alloc * kTabPitch; e += 1024) G[e] = 0.f;
+  wlm_build_T<CPT>(w, T, ow * 8);
+
+  uint32_t stg[kStage];
+  double kst = 0.0;
+#define XPG_MC_ROWS_LOAD(TT)                                                            \
+  {                                                                                     \
+    const int64_t r0_ = (TT) * batch;                                                   \
+    const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);      \
+    const int n_ = B_ * ow;                                                             \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      const int ee_ = e_ < n_ ? e_ : (n_ > 0 ? n_ - 1 : 0);                             \
+      const int rr_ = ow > 0 ? ee_ / ow : 0;                                            \
+      const uint32_t x_ = ow > 0 ? bits[(r0_ + rr_) * words + w_lo + (ee_ - rr_ * ow)] : 0u; \
+      stg[q] = e_ < n_ ? x_ : 0u;                                                       \
+    }                                                                                   \
+    const double k_ = kern[r0_ + (tid < B_ ? tid : B_ - 1)];                            \
+    kst = tid < B_ ? k_ : 0.0;                                                          \
+  }
+#define XPG_MC_ROWS_STORE(TT)                                                           \
+  {                                                                                     \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      if (e_ < batch * ow) Rb[(e_ / ow) * rp + (e_ % ow)] = stg[q];                     \
+    }                                                                                   \
+    const int64_t r0_ = (TT) * batch;                                                   \
+    const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);      \
+    if (tid < batch) kbuf[tid] = kst;                                                   \
+    for (int e_ = tid + 1024; e_ < B_; e_ += 1024) kbuf[e_] = kern[r0_ + e_];           \
+  }
+#define XPG_MC_COLS_LOAD(TT)                                                            \
+  {                                                                                     \
+    const uint32_t* src_ = colbits + ((TT) * cols + c_lo) * bw;                         \
+    const int n_ = ncol * bw;                                                           \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      const uint32_t x_ = n_ > 0 ? src_[e_ < n_ ? e_ : n_ - 1] : 0u;                    \
+      stg[q] = e_ < n_ ? x_ : 0u;                                                       \
+    }                                                                                   \
+  }
+#define XPG_MC_COLS_STORE()                                                             \
+  {                                                                                     \
+    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+      const int e_ = q * 1024 + tid;                                                    \
+      if (e_ < ncol * bw) Cb[(e_ / bw) * cp + (e_ % bw)] = stg[q];                      \
+    }                                                                                   \
+  }
+  XPG_MC_ROWS_LOAD(0)
+  XPG_MC_ROWS_STORE(0)
+  __syncthreads();
+#ifdef XPG_WLM_STAMPS
+  uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
+#endif
+
+  for (int64_t t = 0; t < nsteps; ++t) {
+    const int64_t r0 = t * batch;
+    const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+    const WlmStep sc = stp[t];
+    XPG_MC_COLS_LOAD(t)
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int i = tid + c * 1024;
+      if (i < ncol) w_hist[t * cols + i] = w[c];
+    }
+    // ---- B: partial predictions over the own words (lanes = rows)
+    for (int it = wave; it < nrb * n_bs; it += 16) {
+      const int rb = it % nrb, sl = it / nrb;
+      const int j = rb * 64 + lane;
+      const int wd0 = sl * bsw, wd1 = min(ow, wd0 + bsw);
+      float s = 0.f;
+      if (j < B) {
+        const uint32_t* row = Rb + j * rp;
+        for (int k0 = wd0; k0 < wd1; k0 += 2) {
+          uint32_t wv[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int wd = k0 + h;
+            wv[h] = row[wd < wd1 ? wd : wd0];
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int wd = k0 + h;
+            const float x = nib8(T + ((wd < wd1 ? wd : wd0) * 8) * kTabPitch, wv[h]);
+            s += wd < wd1 ? x : 0.f;
+          }
+        }
+      }
+      if (j < batch) bpart[sl * batch + j] = s;
+    }
+    XPG_STAMP(0)
+    __syncthreads();
+    XPG_STAMP(1)
+    // ---- exchange: publish this slice's partial p_j as 8-byte {value, step tag} granules
+    // (write-through sc1 stores; parity double-buffered), then poll every slice's granule of
+    // row j until it carries this step's tag
+    uint64_t* xs = xp + (t & 1) * P * (int64_t)batch;
+    const uint32_t tag = static_cast<uint32_t>(t + 1);
+    for (int j = tid; j < B; j += 1024) {
+      float p = 0.f;
+      for (int sl = 0; sl < n_bs; ++sl) p += bpart[sl * batch + j];
+      st64_sc1(xs + part * (int64_t)batch + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(p));
+    }
+    XPG_MC_COLS_STORE()
+    XPG_STAMP(2)
+    XPG_STAMP(3)
+    // ---- gather the P partials of every row (thread per (slice, row) granule) ...
+    for (int e = tid; e < P * B; e += 1024) {
+      const int q = e / B, j = e - q * B;
+      const uint64_t* src = xs + q * (int64_t)batch + j;
+      uint64_t gr = ld64_sc1(src);
+      uint32_t n = 0;
+      while (static_cast<uint32_t>(gr >> 32) != tag) {
+        __builtin_amdgcn_s_sleep(1);
+        gr = ld64_sc1(src);
+        if (++n > kMcSpinLimit) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      xv[q * batch + j] = __uint_as_float(static_cast<uint32_t>(gr));
+    }
+    __syncthreads();
+    // ... p_j = their sum in slice order (identical in every workgroup), g_j
+    {
+      const double cg = 2.0 / (static_cast<double>(B) * sc.ksum);
+      for (int j = tid; j < B; j += 1024) {
+        float p = 0.f;
+        for (int q = 0; q < P; ++q) p += xv[q * batch + j];
+        if (part == 0) p_hist[r0 + j] = p;
+        pg[j] = static_cast<float>(kbuf[j] * cg * (static_cast<double>(p) - sc.ybar));
+      }
+    }
+    XPG_STAMP(4)
+    __syncthreads();
+    {
+      const int ngrp = (B + 3) >> 2;
+      for (int e = tid; e < ngrp * 16; e += 1024) {
+        const int grp = e >> 4, vv = e & 15;
+        float acc = 0.f;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int j = 4 * grp + b;
+          acc += ((vv >> b) & 1) && j < B ? pg[j] : 0.f;
+        }
+        G[grp * kTabPitch + vv] = acc;
+      }
+    }
+    __syncthreads();  // G and Cb(t) complete; Rb, kbuf free
+    XPG_STAMP(5)
+    if (t + 1 < nsteps) XPG_MC_ROWS_LOAD(t + 1)
+    // ---- D: gradient of the own columns (lanes = columns)
+    for (int it = wave; it < ncb * n_ds; it += 16) {
+      const int cbk = it % ncb, sl = it / ncb;
+      const int i = cbk * 64 + lane;
+      const int k0 = sl * dsw, k1 = min(bw, k0 + dsw);
+      float s = 0.f;
+      if (i < ncol) {
+        const uint32_t* cb = Cb + i * cp;
+        for (int kk = k0; kk < k1; kk += 2) {
+          uint32_t wv[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = kk + h;
+            wv[h] = cb[k < k1 ? k : k0];
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = kk + h;
+            const float x = nib8(G + ((k < k1 ? k : k0) * 8) * kTabPitch, wv[h]);
+            s += k < k1 ? x : 0.f;
+          }
+        }
+      }
+      if (i < cpad) dpart[sl * cpad + i] = s;
+    }
+    __syncthreads();
+    XPG_STAMP(6)
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int i = tid + c * 1024;
+      if (i < ncol) {
+        float s = 0.f;
+        for (int sl = 0; sl < n_ds; ++sl) s += dpart[sl * cpad + i];
+        const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
+        float g = fmaf(l1s, sg, s);
+        g = fmaf(Pm.weight_decay, w[c], g);
+        m[c] = fmaf(1.f - Pm.beta1, g - m[c], m[c]);
+        v[c] = fmaf(1.f - Pm.beta2, g * g, v[c] * Pm.beta2);
+        const float denom = sqrtf(v[c]) / sc.bc2_sqrt + Pm.eps;
+        w[c] = w[c] - sc.step_size * (m[c] / denom);
+      }
+    }
+    wlm_build_T<CPT>(w, T, ow * 8);
+    if (t + 1 < nsteps) XPG_MC_ROWS_STORE(t + 1)
+    __syncthreads();
+    XPG_STAMP(7)
+  }
+#ifdef XPG_WLM_STAMPS
+  if (blockIdx.x == 0 && (tid == 0 || tid == 1023)) {
+    for (int k = 0; k < 8; ++k) g_wlm_stamps[tid == 0 ? 0 : 1][k] = stamp_acc[k];
+  }
+#endif
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int i = tid + c * 1024;
+    if (i < ncol) {
+      wg[i] = w[c];
+      mg[i] = m[c];
+      vg[i] = v[c];
+    }
+  }
+#undef XPG_MC_ROWS_LOAD
+#undef XPG_MC_ROWS_STORE
+#undef XPG_MC_COLS_LOAD
+#undef XPG_MC_COLS_STORE
+}
+
+
 // loss_t = sum_j k_j (p_j - ybar)^2 / (B sum k) + sum_i (y_i - ybar)^2 / B^2 + l1 * mean|w_t|
 __global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hist,
                                                   const float* __restrict__ w_hist,
@@ -1109,6 +1409,221 @@ __global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hi
                 static_cast<double>(reg);
   }
 }
+
+// -------------------------------------------------------------- surrogate, many-column (grid) fit
+// For S beyond the single-workgroup fit (graph_prediction on large graphs, regime (ii)) each
+// Adam step is three grid launches over 2048-column chunks (64 mask words), streaming the step's
+// B x S mask bits from HBM twice (HBM-bound: 2 * B * S / 8 bytes per step):
+//   k_gw_p     per chunk: nibble tables of w in LDS; 64-row tiles staged through LDS, lanes =
+//              rows (one table per lane group: conflict-free); partial p_j per workgroup
+//   k_gw_g     p_j = sum of the partials, g_j = 2 k_j (p_j - ybar) / (B sum k), the loss term
+//   k_gw_grad  per chunk: nibble tables of g in LDS; the tile's bits are transposed by wave
+//              ballots (lane b keeps column b's 64-row mask); (M_b^T g)_i by lookups, then the
+//              Adam update of the chunk's columns and the chunk's sum |w| for the loss
+constexpr int kGwWords = 64;                // mask words per chunk (2048 columns)
+constexpr int kGwThreads = 512;             // 8 waves x 8 words
+constexpr int kGwTilePitch = kGwWords + 1;  // odd pitch: lanes = rows hit distinct banks
+
+__device__ __forceinline__ void gw_load_tile(const uint32_t* __restrict__ bits, int64_t words, int64_t row0,
+                                             int nrows, int64_t w0, int nw, uint32_t* tile) {
+  const int tid = threadIdx.x;
+  const int r = tid >> 3, seg = (tid & 7) * 8;  // 64 rows x 8 segments of 8 words
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int wd = seg + q;
+    uint32_t x = 0u;
+    if (r < nrows && wd < nw) x = bits[(row0 + r) * words + w0 + wd];
+    tile[r * kGwTilePitch + wd] = x;
+  }
+}
+
+__global__ __launch_bounds__(kGwThreads) void k_gw_p(const uint32_t* __restrict__ bits, int64_t rows,
+                                                     int64_t cols, int64_t words, int batch, int64_t t,
+                                                     const float* __restrict__ wg, float* __restrict__ p_part) {
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  float* T = gsm;                                                        // [64*8][17]
+  uint32_t* tile = reinterpret_cast<uint32_t*>(T + kGwWords * 8 * kTabPitch);  // [64][65]
+  float* red = reinterpret_cast<float*>(tile + 64 * kGwTilePitch);      // [8][64]
+  float* pacc = red + 8 * 64;                                            // [batch]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t f = blockIdx.y;
+  bits += f * rows * words;
+  wg += f * cols;
+  p_part += (f * gridDim.x + blockIdx.x) * (int64_t)batch;
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const int64_t n_chunks = (words + kGwWords - 1) / kGwWords;
+  for (int j = tid; j < batch; j += kGwThreads) pacc[j] = 0.f;
+  for (int64_t ck = blockIdx.x; ck < n_chunks; ck += gridDim.x) {
+    const int64_t w0 = ck * kGwWords;
+    const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
+    __syncthreads();  // previous chunk's readers of T are done
+    for (int e = tid; e < kGwWords * 8 * 16; e += kGwThreads) {  // table (word, nibble) entry v
+      const int tb = e >> 4, v = e & 15;
+      const int64_t c = (w0 + (tb >> 3)) * 32 + (tb & 7) * 4;
+      float s = 0.f;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) s += ((v >> b) & 1) && c + b < cols ? wg[c + b] : 0.f;
+      T[tb * kTabPitch + v] = s;
+    }
+    for (int rb = 0; rb * 64 < B; ++rb) {
+      const int nr = min(64, B - rb * 64);
+      __syncthreads();  // tile free
+      gw_load_tile(bits, words, r0 + rb * 64, nr, w0, nw, tile);
+      __syncthreads();
+      float s = 0.f;
+      const uint32_t* row = tile + lane * kGwTilePitch;
+#pragma unroll 2
+      for (int q = 0; q < 8; ++q) {
+        const int wd = wave * 8 + q;
+        s += nib8(T + (wd * 8) * kTabPitch, row[wd]);  // words >= nw are zero -> entry 0 = 0
+      }
+      red[wave * 64 + lane] = s;
+      __syncthreads();
+      if (tid < 64 && tid < nr) {
+        float p = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) p += red[w * 64 + tid];
+        pacc[rb * 64 + tid] += p;
+      }
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < B; j += kGwThreads) p_part[j] = pacc[j];
+}
+
+__global__ __launch_bounds__(256) void k_gw_g(const float* __restrict__ p_part, int n_wg, int64_t rows,
+                                              int batch, int64_t t, const double* __restrict__ kern,
+                                              const WlmStep* __restrict__ stp, int64_t steps,
+                                              float* __restrict__ g, float* __restrict__ p_hist,
+                                              double* __restrict__ tk_part) {
+  __shared__ double red[16];
+  const int64_t f = blockIdx.y;
+  p_part += f * n_wg * (int64_t)batch;
+  kern += f * rows;
+  g += f * batch;
+  p_hist += f * rows;
+  const WlmStep sc = stp[f * steps + t];
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  double tk = 0.0;
+  if (j < B) {
+    float p = 0.f;
+    for (int w = 0; w < n_wg; ++w) p += p_part[(int64_t)w * batch + j];
+    const double kj = kern[r0 + j];
+    const double d = static_cast<double>(p) - sc.ybar;
+    g[j] = static_cast<float>(kj * (2.0 / (static_cast<double>(B) * sc.ksum)) * d);
+    p_hist[r0 + j] = p;
+    tk = kj * d * d;
+  }
+  const double T = block_sum_d(tk, red);
+  if (threadIdx.x == 0) tk_part[(f * steps + t) * gridDim.x + blockIdx.x] = T;
+}
+
+__global__ __launch_bounds__(kGwThreads) void k_gw_grad(const uint32_t* __restrict__ bits, int64_t rows,
+                                                        int64_t cols, int64_t words, int batch, int64_t t,
+                                                        const float* __restrict__ g, const WlmStep* __restrict__ stp,
+                                                        int64_t steps, xpg_wlm_params P, float* __restrict__ wg,
+                                                        float* __restrict__ mg, float* __restrict__ vg,
+                                                        double* __restrict__ aw_part) {
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  __shared__ double red[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t f = blockIdx.y;
+  bits += f * rows * words;
+  g += f * batch;
+  wg += f * cols;
+  mg += f * cols;
+  vg += f * cols;
+  const WlmStep sc = stp[f * steps + t];
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const int ngrp = ((batch + 63) / 64) * 16;  // every 4-row group of every 64-row tile
+  float* G = gsm;                                                        // [ngrp][17]
+  uint32_t* tile = reinterpret_cast<uint32_t*>(G + ((ngrp * kTabPitch + 3) & ~3));  // [64][65]
+  for (int e = tid; e < ngrp * 16; e += kGwThreads) {
+    const int grp = e >> 4, v = e & 15;
+    float s = 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = 4 * grp + b;
+      s += ((v >> b) & 1) && j < B ? g[j] : 0.f;
+    }
+    G[grp * kTabPitch + v] = s;
+  }
+  const float l1s = P.l1_lambda / static_cast<float>(cols);
+  const int64_t n_chunks = (words + kGwWords - 1) / kGwWords;
+  double aw = 0.0;
+  for (int64_t ck = blockIdx.x; ck < n_chunks; ck += gridDim.x) {
+    const int64_t w0 = ck * kGwWords;
+    const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int rb = 0; rb * 64 < B; ++rb) {
+      const int nr = min(64, B - rb * 64);
+      __syncthreads();  // tile free (and G complete on the first pass)
+      gw_load_tile(bits, words, r0 + rb * 64, nr, w0, nw, tile);
+      __syncthreads();
+      const uint32_t* row = tile + lane * kGwTilePitch;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int wd = wave * 8 + 2 * q;
+        const uint32_t x0 = row[wd], x1 = row[wd + 1];
+        uint32_t lo = 0u, hi = 0u;  // this lane's column: 64-row mask (rows rb*64 + 0..63)
+#pragma unroll
+        for (int b = 0; b < 32; ++b) {
+          const uint64_t m0 = __ballot((x0 >> b) & 1u);
+          const uint64_t m1 = __ballot((x1 >> b) & 1u);
+          const uint64_t m = (lane & 31) == b ? ((lane >> 5) ? m1 : m0) : 0ull;
+          lo |= static_cast<uint32_t>(m);
+          hi |= static_cast<uint32_t>(m >> 32);
+        }
+        const float* gt = G + (rb * 16) * kTabPitch;
+        acc[q] += nib8(gt, lo) + nib8(gt + 8 * kTabPitch, hi);
+      }
+    }
+    // Adam on this chunk's columns: lane < 32 -> word wd, lane >= 32 -> word wd + 1
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t c = (w0 + wave * 8 + 2 * q + (lane >> 5)) * 32 + (lane & 31);
+      if (c < cols) {
+        float w = wg[c], m = mg[c], v = vg[c];
+        aw += fabs(static_cast<double>(w));
+        const float sgn = w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f);
+        float gr = fmaf(l1s, sgn, acc[q]);
+        gr = fmaf(P.weight_decay, w, gr);
+        m = fmaf(1.f - P.beta1, gr - m, m);
+        v = fmaf(1.f - P.beta2, gr * gr, v * P.beta2);
+        const float denom = sqrtf(v) / sc.bc2_sqrt + P.eps;
+        w = w - sc.step_size * (m / denom);
+        wg[c] = w;
+        mg[c] = m;
+        vg[c] = v;
+      }
+    }
+  }
+  const double A = block_sum_d(aw, red);
+  if (tid == 0) aw_part[(f * steps + t) * gridDim.x + blockIdx.x] = A;
+}
+
+__global__ __launch_bounds__(64) void k_gw_loss(const double* __restrict__ tk_part, int n_tk,
+                                                const double* __restrict__ aw_part, int n_aw,
+                                                const WlmStep* __restrict__ stp, int64_t rows, int64_t cols,
+                                                int batch, float l1, double* __restrict__ losses) {
+  const int64_t t = blockIdx.x, steps = gridDim.x, f = blockIdx.y;
+  if (threadIdx.x != 0) return;
+  const int64_t k = f * steps + t;
+  const WlmStep sc = stp[k];
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  double Tk = 0.0, Sa = 0.0;
+  for (int i = 0; i < n_tk; ++i) Tk += tk_part[k * n_tk + i];
+  for (int i = 0; i < n_aw; ++i) Sa += aw_part[k * n_aw + i];
+  const float reg = l1 * static_cast<float>(Sa / cols);
+  losses[k] = Tk / (static_cast<double>(B) * sc.ksum) + sc.vy / (static_cast<double>(B) * B) +
+              static_cast<double>(reg);
+}
+
 
 __global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t* __restrict__ out) {
   if (threadIdx.x != 0) return;
@@ -1206,8 +1721,9 @@ int launch_agg(const AggArgs& a, hipStream_t st) {
 
 // Fused single-launch forward when the plan fits (returns 1 when it does not apply).
 int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
+  // opt-in while the per-row latency chains make it slower than the multi-kernel path at c2
   const char* env = getenv("XPG_FORWARD");
-  if (env && std::strcmp(env, "unfused") == 0) return 1;
+  if (!env || std::strcmp(env, "fused") != 0) return 1;
   if (p->n_layers > kFusedMaxLayers || p->n_head > kFusedMaxHead) return 1;
   FusedArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1491,7 +2007,32 @@ struct WlmWs {
   int bw, n_bs, n_ds;
   bool stage;
   size_t lds;
+  // multi-workgroup fit
+  bool mc, xcd;
+  int P, wpp, mc_bs, mc_ds;
+  size_t xp_off, cnt_off, lds_mc;
+  // grid (many-column) fit
+  bool grid;
+  int n_wg, n_tk;
+  size_t ppart_off, g_off, tk_off, aw_off, lds_p, lds_g;
 };
+
+static bool wlm_env(const char* v) {
+  const char* env = getenv("XPG_WLM");
+  return env && std::strcmp(env, v) == 0;
+}
+static bool wlm_force_grid() { return wlm_env("grid"); }
+
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 1;
+  }
+  return cus;
+}
 
 // Word slices per wave item: minimise (rounds of 16 waves) x (words per item + 1 for the item's
 // fixed cost) over blocks x slices items.
@@ -1508,10 +2049,40 @@ static int wlm_slices(int64_t blocks, int words) {
   return best;
 }
 
+static int wlm_layout_grid(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
+  const int64_t steps = cdiv(rows, batch);
+  const int64_t words = cdiv(cols, 32);
+  XPG_REQ(batch <= 8192, "wlm_fit: batch > 8192 rows is not supported by the many-column fit");
+  L->grid = true;
+  L->stage = false;
+  L->n_wg = static_cast<int>(std::min<int64_t>(cdiv(words, kGwWords), 512));
+  L->n_tk = static_cast<int>(cdiv(batch, 256));
+  L->lds_p = sizeof(float) * (size_t)(kGwWords * 8 * kTabPitch + 64 * kGwTilePitch + 8 * 64 + batch);
+  L->lds_g = sizeof(float) * (size_t)((((batch + 63) / 64) * 16 * kTabPitch + 3) & ~3) +
+             sizeof(uint32_t) * 64 * kGwTilePitch;
+  const size_t F = static_cast<size_t>(n_fits);
+  size_t off = 0;
+  L->steps_off = off;
+  off += align_up(F * sizeof(WlmStep) * (size_t)steps);
+  L->ppart_off = off;
+  off += align_up(F * sizeof(float) * (size_t)L->n_wg * batch);
+  L->g_off = off;
+  off += align_up(F * sizeof(float) * (size_t)batch);
+  L->phist_off = off;
+  off += align_up(F * sizeof(float) * (size_t)rows);
+  L->tk_off = off;
+  off += align_up(F * sizeof(double) * (size_t)steps * L->n_tk);
+  L->aw_off = off;
+  off += align_up(F * sizeof(double) * (size_t)steps * L->n_wg);
+  L->total = off;
+  return XPG_OK;
+}
+
 static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
   XPG_REQ(n_fits > 0 && rows > 0 && cols > 0 && batch > 0, "wlm_fit: bad arguments");
-  XPG_REQ(cols <= 16 * 1024, "wlm_fit: more than 16384 columns is not supported by the single-workgroup fit");
   XPG_REQ(batch <= 1 << 20, "wlm_fit: batch too large");
+  L->grid = false;
+  if (cols > 16 * 1024 || wlm_force_grid()) return wlm_layout_grid(n_fits, rows, cols, batch, L);
   const int64_t steps = cdiv(rows, batch);
   const int words = words_of(cols);
   L->bw = static_cast<int>(cdiv(batch, 32));
@@ -1533,6 +2104,34 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   L->stage = g_bytes() + t_bytes + stage_bytes <= lds_cap && (int64_t)batch * words <= kStage * 1024 &&
              cols * (int64_t)L->bw <= kStage * 1024;
   L->lds = g_bytes() + (L->stage ? t_bytes + stage_bytes : 0);
+  // multi-workgroup fit: P workgroups (one per CU, all co-resident) per fit
+  L->mc = false;
+  if (!wlm_env("single") && (words >= 8 || wlm_env("mc"))) {
+    const char* xe = getenv("XPG_MC_XCD");
+    L->xcd = !(xe && std::strcmp(xe, "0") == 0);
+    int P = std::min(kMcMaxP, std::max(2, words / 4));
+    while (P > 1 && (L->xcd ? cdiv(n_fits, 8) * P > device_cus() / 8 : n_fits * P > device_cus())) --P;
+    if (P >= 2) {
+      const int wpp = static_cast<int>(cdiv(words, P));
+      P = static_cast<int>(cdiv(words, wpp));
+      const int bs = wlm_slices(cdiv(batch, 64), wpp);
+      const int ds = wlm_slices(cdiv((int64_t)wpp * 32, 64), L->bw);
+      const int64_t cpad = ((int64_t)wpp * 32 + 63) & ~int64_t(63);
+      const size_t fl = sizeof(float) *
+                        (size_t)((L->bw * 8 * kTabPitch + bs * batch + ds * cpad + batch + P * batch + 1) & ~int64_t(1));
+      const size_t lds = fl + sizeof(double) * (size_t)batch + sizeof(float) * (size_t)wpp * 8 * kTabPitch +
+                         sizeof(uint32_t) * ((size_t)batch * (wpp | 1) + (size_t)wpp * 32 * (L->bw | 1));
+      if (P >= 2 && lds <= lds_cap && (int64_t)batch * wpp <= kStage * 1024 &&
+          (int64_t)wpp * 32 * L->bw <= kStage * 1024) {
+        L->mc = true;
+        L->P = P;
+        L->wpp = wpp;
+        L->mc_bs = bs;
+        L->mc_ds = ds;
+        L->lds_mc = std::max<size_t>(lds, 81 * 1024);  // > half the CU's LDS: one workgroup per CU
+      }
+    }
+  }
   const size_t F = static_cast<size_t>(n_fits);
   size_t off = 0;
   L->steps_off = off;
@@ -1545,7 +2144,51 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   off += align_up(F * sizeof(float) * (size_t)steps * cols);
   L->tglob_off = off;
   off += align_up(L->stage ? 0 : F * t_bytes);
+  L->xp_off = off;
+  off += align_up(L->mc ? F * sizeof(uint64_t) * 2 * L->P * (size_t)batch : 0);
+  L->cnt_off = off;
+  off += align_up(sizeof(uint32_t) * (F + 1));
   L->total = off;
+  return XPG_OK;
+}
+
+static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                        const float* y, const double* kernel, const xpg_wlm_params& P, int64_t step0, float* w,
+                        float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, char* ws,
+                        const WlmWs& L, hipStream_t st) {
+  const int64_t steps = cdiv(rows, batch);
+  const int64_t words = cdiv(cols, 32);
+  const int ib = static_cast<int>(batch);
+  const unsigned nf = static_cast<unsigned>(n_fits);
+  WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
+  float* p_part = reinterpret_cast<float*>(ws + L.ppart_off);
+  float* g = reinterpret_cast<float*>(ws + L.g_off);
+  float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
+  double* tk_part = reinterpret_cast<double*>(ws + L.tk_off);
+  double* aw_part = reinterpret_cast<double*>(ws + L.aw_off);
+  hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib, P,
+                     step0, stp);
+  XPG_LAUNCHED();
+  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gw_p), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(L.lds_p)));
+  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gw_grad),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_g)));
+  const dim3 gw(static_cast<unsigned>(L.n_wg), nf);
+  for (int64_t t = 0; t < steps; ++t) {
+    hipLaunchKernelGGL(k_gw_p, gw, dim3(kGwThreads), L.lds_p, st, bits, rows, cols, words, ib, t, w, p_part);
+    XPG_LAUNCHED();
+    hipLaunchKernelGGL(k_gw_g, dim3(static_cast<unsigned>(L.n_tk), nf), dim3(256), 0, st, p_part, L.n_wg, rows, ib,
+                       t, kernel, stp, steps, g, p_hist, tk_part);
+    XPG_LAUNCHED();
+    hipLaunchKernelGGL(k_gw_grad, gw, dim3(kGwThreads), L.lds_g, st, bits, rows, cols, words, ib, t, g, stp, steps,
+                       P, w, adam_m, adam_v, aw_part);
+    XPG_LAUNCHED();
+  }
+  hipLaunchKernelGGL(k_gw_loss, dim3(static_cast<unsigned>(steps), nf), dim3(64), 0, st, tk_part, L.n_tk, aw_part,
+                     L.n_wg, stp, rows, cols, ib, P.l1_lambda, losses);
+  XPG_LAUNCHED();
+  hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch);
+  XPG_LAUNCHED();
   return XPG_OK;
 }
 
@@ -1570,6 +2213,8 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   hipStream_t st = S(stream);
   char* ws = static_cast<char*>(workspace);
   WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
+  if (L.grid) return wlm_fit_grid(n_fits, bits, rows, cols, batch, y, kernel, *params, step0, w, adam_m, adam_v,
+                                  losses, best_epoch, ws, L, st);
   uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
   float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
   float* w_hist = reinterpret_cast<float*>(ws + L.whist_off);
@@ -1585,22 +2230,44 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(waves, 4)), nf), dim3(256), 0, st, bits, rows,
                      ic, words, ib, L.bw, steps, colbits);
   XPG_LAUNCHED();
+  bool launched = false;
+  if (L.mc) {
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(ws + L.cnt_off);
+    uint64_t* xp = reinterpret_cast<uint64_t*>(ws + L.xp_off);
+    // granule tags restart at 1 every call: clear the exchange slots and the error word
+    XPG_HIP(hipMemsetAsync(xp, 0, sizeof(uint64_t) * 2 * L.P * (size_t)batch * n_fits, st));
+    XPG_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n_fits + 1), st));
+    const int cpt_mc = static_cast<int>(cdiv((int64_t)L.wpp * 32, 1024));
+    const dim3 grid(static_cast<unsigned>(L.xcd ? 8 * L.P * cdiv(n_fits, 8) : n_fits * L.P));
+#define XPG_WLM_MC(C)                                                                                       \
+    if (!launched && cpt_mc <= C) {                                                                         \
+      XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit_mc<C>),                          \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_mc))); \
+      hipLaunchKernelGGL(k_wlm_fit_mc<C>, grid, dim3(1024), L.lds_mc, st, bits, colbits, rows, ic, words, ib, L.bw, \
+                         L.P, L.wpp, L.mc_bs, L.mc_ds, n_fits, L.xcd ? 1 : 0, kernel, stp, *params, w, adam_m,    \
+                         adam_v, p_hist, w_hist, xp, cnt + n_fits);                                         \
+      XPG_LAUNCHED();                                                                                       \
+      launched = true;                                                                                      \
+    }
+    XPG_WLM_MC(1) XPG_WLM_MC(2) XPG_WLM_MC(4)
+#undef XPG_WLM_MC
+    if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported slice width");
+  }
   const int cpt = static_cast<int>(cdiv(cols, 1024));
 #define XPG_WLM(C, TL)                                                                                     \
-  if (cpt <= C && L.stage == TL) {                                                                      \
+  if (!launched && cpt <= C && L.stage == TL) {                                                                      \
     XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit<C, TL>),                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds)));     \
     hipLaunchKernelGGL((k_wlm_fit<C, TL>), dim3(nf), dim3(1024), L.lds, st, bits, colbits, rows, ic, words, \
                        ib, L.bw, L.n_bs, L.n_ds, kernel, stp, *params, w, adam_m, adam_v, p_hist, w_hist,  \
                        t_glob);                                                                            \
     XPG_LAUNCHED();                                                                                        \
-    goto fitted;                                                                                           \
+    launched = true;                                                                                       \
   }
   XPG_WLM(1, true) XPG_WLM(2, true) XPG_WLM(4, true) XPG_WLM(8, true) XPG_WLM(16, true)
   XPG_WLM(1, false) XPG_WLM(2, false) XPG_WLM(4, false) XPG_WLM(8, false) XPG_WLM(16, false)
 #undef XPG_WLM
-  return fail(XPG_EINVAL, "wlm_fit: unsupported column count");
-fitted:
+  if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported column count");
   hipLaunchKernelGGL(k_wlm_loss, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, p_hist, w_hist, kernel,
                      stp, rows, ic, ib, params->l1_lambda, losses);
   XPG_LAUNCHED();

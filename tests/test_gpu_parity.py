@@ -31,12 +31,9 @@ def _eng():
 
 @pytest.fixture(params=["fused", "unfused"])
 def fwd_path(request, monkeypatch):
-    """xpg_masked_forward has two HIP paths: the single-launch fused kernel (plans that fit in
-    LDS) and the multi-kernel path; XPG_FORWARD=unfused forces the latter."""
-    if request.param == "unfused":
-        monkeypatch.setenv("XPG_FORWARD", "unfused")
-    else:
-        monkeypatch.delenv("XPG_FORWARD", raising=False)
+    """xpg_masked_forward has two HIP paths: the multi-kernel path (default) and the
+    single-launch fused kernel for plans that fit in LDS (XPG_FORWARD=fused)."""
+    monkeypatch.setenv("XPG_FORWARD", request.param)
     return request.param
 
 
@@ -185,8 +182,11 @@ def test_generic_path_matches_engine():
 
 
 # ------------------------------------------------------------------ surrogate
+@pytest.mark.parametrize("wlm_path", ["auto", "mc"])
 @pytest.mark.parametrize("name", CASES)
-def test_wlm_fit_vs_reference(name):
+def test_wlm_fit_vs_reference(name, wlm_path, monkeypatch):
+    if wlm_path != "auto":
+        monkeypatch.setenv("XPG_WLM", wlm_path)
     e = _eng()
     z, meta = load_case(name)
     for i, m in enumerate(repeat_masks(z, meta)):
@@ -205,8 +205,12 @@ def test_wlm_fit_vs_reference(name):
                                    (3000, 1193, 256),   # short last batch (quirk Q7)
                                    (2000, 700, 100),    # batch not a multiple of 32
                                    (640, 4100, 64)])    # > 4096 columns
-def test_wlm_fit_vs_oracle_large(R, S, B):
-    """Fresh data vs the fp64 oracle at sizes the golden fixtures do not reach."""
+@pytest.mark.parametrize("wlm_path", ["single", "mc", "grid"])
+def test_wlm_fit_vs_oracle_large(R, S, B, wlm_path, monkeypatch):
+    """Fresh data vs the fp64 oracle at sizes the golden fixtures do not reach, through each of
+    the three fit kernels: one workgroup per fit (XPG_WLM=single), P co-resident workgroups per
+    fit (mc, the default from 256 columns) and the many-column grid fit (S > 16384)."""
+    monkeypatch.setenv("XPG_WLM", wlm_path)
     e = _eng()
     rng = np.random.default_rng(11)
     m = rng.random((R, S)) < 0.5
@@ -222,11 +226,35 @@ def test_wlm_fit_vs_oracle_large(R, S, B):
     np.testing.assert_allclose(losses.cpu().numpy(), rl, rtol=1e-5)
 
 
-def test_wlm_fit_batched_independent_fits():
-    """n_fits independent surrogates in one launch (one workgroup each) == separate fits."""
+def test_wlm_fit_many_columns_vs_oracle():
+    """S = 40,000 columns (> 16384: the grid fit), two independent fits in one call."""
+    e = _eng()
+    rng = np.random.default_rng(3)
+    F, R, S, B = 2, 768, 40_000, 256
+    m = rng.random((F, R, S)) < 0.5
+    y = rng.random((F, R)).astype(np.float32)
+    k = np.stack([oracle.shap_kernel(m[f]) for f in range(F)])
+    w0 = ((rng.random((F, S)) - 0.5) * 0.01).astype(np.float32)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    bits = torch.stack([e.pack_masks(torch.as_tensor(m[f]).to(DEV)) for f in range(F)])
+    w, losses, best, _, _ = e.wlm_fit(bits, S, B, torch.as_tensor(y), torch.as_tensor(k),
+                                      torch.as_tensor(w0), params)
+    for f in range(F):
+        ref, rl, rb = oracle.train_wlm(m[f], B, y[f], k[f], w0[f], params)
+        np.testing.assert_allclose(w[f].cpu().numpy(), ref, rtol=0, atol=1e-4)
+        np.testing.assert_allclose(losses[f].cpu().numpy(), rl, rtol=1e-5)
+        assert int(best[f]) == rb
+
+
+@pytest.mark.parametrize("F,S", [(5, 200), (11, 700)])
+@pytest.mark.parametrize("wlm_path", ["single", "mc"])
+def test_wlm_fit_batched_independent_fits(wlm_path, F, S, monkeypatch):
+    """n_fits independent surrogates in one launch == separate fits (F = 11 spans two groups of
+    the multi-workgroup fit's XCD-local block mapping)."""
+    monkeypatch.setenv("XPG_WLM", wlm_path)
     e = _eng()
     rng = np.random.default_rng(5)
-    F, R, S, B = 5, 1002, 200, 20
+    R, B = 1002, 20
     m = rng.random((F, R, S)) < 0.5
     y = rng.random((F, R)).astype(np.float32)
     k = np.stack([oracle.shap_kernel(m[f]) for f in range(F)])
@@ -349,5 +377,5 @@ def test_c2_scale_forward_properties(fwd_path):
         try:
             y3 = plan.forward(bits)[:, 0]
         finally:
-            del os.environ["XPG_FORWARD"]
+            os.environ["XPG_FORWARD"] = "fused"
         torch.testing.assert_close(y3, y, rtol=0, atol=2e-6)

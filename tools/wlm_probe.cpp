@@ -3,6 +3,8 @@
 #include "../bikg_graph_explainability_public_amd/csrc/xpgnn.hip"
 
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -46,7 +48,10 @@ int main(int argc, char** argv) {
     const int64_t steps = (R + batch - 1) / batch;
     printf("S=%ld R=%ld batch=%ld: fit chain %.1f us (%.2f us/step); cycles/step per segment:\n", (long)S, (long)R,
            (long)batch, ms * 1e3, ms * 1e3 / steps);
-    const char* nm[8] = {"B lookups", "syncA", "G + COLS_ST", "sync1", "D lookups", "syncD", "Adam+T+ROWS", "sync2"};
+    const bool mc = getenv("XPG_WLM") == nullptr || strcmp(getenv("XPG_WLM"), "single") != 0;
+    const char* nm1[8] = {"B lookups", "syncA", "G + COLS_ST", "sync1", "D lookups", "syncD", "Adam+T+ROWS", "sync2"};
+    const char* nm2[8] = {"B lookups", "syncA", "publish+COLS", "bar+signal+poll", "p sum + g", "G build+bar", "D + bar", "Adam+T+ROWS+bar"};
+    const char* const* nm = mc ? nm2 : nm1;
     for (int q = 0; q < 8; ++q) printf("  %-12s wave0 %8.0f  last %8.0f\n", nm[q], (double)st[0][q] / steps, (double)st[1][q] / steps);
   }
   return 0;
