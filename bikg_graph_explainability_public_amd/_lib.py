@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -30,7 +30,8 @@ class TermDesc(ctypes.Structure):
 
 class LayerDesc(ctypes.Structure):
     _fields_ = [("n_terms", c_i32), ("act", c_i32), ("f_in_pad", c_i32), ("f_out", c_i32),
-                ("f_out_pad", c_i32), ("n_tgt", c_i32), ("tgt_prev", c_vp), ("tgt_f0", c_vp),
+                ("f_out_pad", c_i32), ("n_tgt", c_i32), ("n_edges", c_i32), ("tgt_prev", c_vp),
+                ("tgt_f0", c_vp),
                 ("agg_ptr", c_vp), ("agg_src", c_vp), ("agg_f0", c_vp), ("self_mult", c_vp),
                 ("terms", TermDesc * MAX_TERMS), ("weight", c_vp), ("bias", c_vp)]
 
@@ -42,7 +43,7 @@ class HeadDesc(ctypes.Structure):
 
 class ForwardPlanDesc(ctypes.Structure):
     _fields_ = [("cols", c_i64), ("n_rel", c_i32), ("n0", c_i32), ("f0_node", c_vp),
-                ("deg_ptr", c_vp), ("deg_src", c_vp), ("n_layers", c_i32),
+                ("deg_ptr", c_vp), ("deg_src", c_vp), ("n_deg_edges", c_i64), ("n_layers", c_i32),
                 ("layers", ctypes.POINTER(LayerDesc)), ("n_head", c_i32),
                 ("head", ctypes.POINTER(HeadDesc)), ("out_col", c_i32)]
 
@@ -76,11 +77,13 @@ EXPORTED = tuple(_SIGS.keys())
 _lib = None
 
 
-def load(path=LIB_PATH):
-    """Load (once) and type the native library; raise NativeLibraryError if unavailable."""
+def load(path=None):
+    """Load (once) and type the native library; raise NativeLibraryError if unavailable.
+    XPG_LIB overrides the path (diagnostic builds, e.g. tools/build_stamps.sh)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("XPG_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise NativeLibraryError(
             f"{path} not found: the HIP engine is not built (run __graft_entry__.build()); "

@@ -674,6 +674,447 @@ __global__ __launch_bounds__(WPB * 64) void k_fused_forward(const FusedArgs a) {
   }
 }
 
+#ifdef XPG_WLM_STAMPS  // diagnostic build only (tools/wlm_probe.cpp): per-phase cycle counts
+#define XPG_STAMP(k)                                                       \
+  {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();                    \
+    stamp_acc[k] += now_ - stamp_last;                                     \
+    stamp_last = now_;                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+  }
+__device__ uint64_t g_wlm_stamps[2][8];
+#else
+#define XPG_STAMP(k)
+#endif
+
+// ------------------------------------------------------------- fused forward, lanes = mask rows
+// For plans of one or two conv layers (the query's receptive field): one 1024-thread workgroup
+// per 64 mask rows, lane = row.  The 16 waves split the F_0 nodes for the degree pass and the
+// feature columns (FS = f1_pad / 16 each) for the layer passes.  Control flow and every index
+// are uniform across a wave: CSR arrays sit in LDS and are pulled 64 at a time into a VGPR and
+// handed out with v_readlane; the per-lane work is mask-word tests, one kept/degree factor per
+// edge (dv = 1/sqrt(1+kin) of kept nodes, computed once per node and row) and FS FMAs against
+// broadcast LDS reads of the layer-1 table row.  Layer-1 outputs are recomputed for each layer-2
+// use instead of stored (a single-query plan uses each once); the layer-2 aggregate stays in
+// registers until the wave-split dense layer and head.
+struct RowsFwdArgs {
+  int64_t rows;
+  const uint32_t* bits;
+  float* y;
+  int words, n0, n_rel, n_layers, out_col, n_last, n_deg_edges, n1_edges, n2_edges;
+  const int32_t* f0_node;
+  const int32_t* deg_ptr;
+  const int32_t* deg_src;
+  // layer 1 (tables in LDS)
+  int n1, n_terms1, act1, f1_out, f1_pad;
+  const int32_t* l1_ptr;
+  const int32_t* l1_f0;
+  const int32_t* l1_smul;
+  const int32_t* l1_tgt_f0;
+  int kind1[XPG_MAX_TERMS], rel1[XPG_MAX_TERMS];
+  const float* tab1[XPG_MAX_TERMS];
+  const float* bias1;
+  // layer 2 (aggregate then dense)
+  int n2, n_terms2, act2, f2_out, f2_pad;
+  const int32_t* l2_ptr;
+  const int32_t* l2_src;
+  const int32_t* l2_f0;
+  const int32_t* l2_smul;
+  const int32_t* l2_tgt_f0;
+  const int32_t* l2_tgt_prev;
+  int kind2[XPG_MAX_TERMS], rel2[XPG_MAX_TERMS];
+  const float* w2;
+  const float* bias2;
+  int n_head;
+  FusedHead H[kFusedMaxHead];
+  // LDS image (4-byte units)
+  int stage_bits, mb_pitch, w2_lds, o_tab, o_mb, o_dv, o_kt, o_a2, o_h0, o_h1, o_w2;
+  int o_dptr, o_f0n, o_dsrc, o_l1ptr, o_l1f0, o_l1smul, o_l1tgt, o_l2ptr, o_l2src, o_l2f0, o_l2smul, o_l2tgt, o_l2prev;
+  int o_hw[kFusedMaxHead];  // head weights in LDS (-1: read from global)
+};
+
+constexpr int kRowsWaves = 16;
+
+__device__ __forceinline__ int rdl(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+
+__device__ __forceinline__ uint32_t row_word(const RowsFwdArgs& a, const uint32_t* mb, int64_t row, int lane,
+                                             int node) {
+  return a.stage_bits ? mb[lane * a.mb_pitch + (node >> 5)] : a.bits[row * a.words + (node >> 5)];
+}
+
+template <int FS>
+__device__ __forceinline__ void ld_fs(const float* p, float (&v)[FS]) {
+  if constexpr (FS % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < FS / 4; ++i) {
+      const float4 x = reinterpret_cast<const float4*>(p)[i];
+      v[4 * i] = x.x;
+      v[4 * i + 1] = x.y;
+      v[4 * i + 2] = x.z;
+      v[4 * i + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < FS / 2; ++i) {
+      const float2 x = reinterpret_cast<const float2*>(p)[i];
+      v[2 * i] = x.x;
+      v[2 * i + 1] = x.y;
+    }
+  }
+}
+
+// out[o][lane] = act(sum_k A[k][lane] W[o][k] + b[o]) for o < n_pad (0 beyond n_real); wave w
+// takes outputs w, w + 16, ...  W rows are wave-uniform (broadcast) reads; K % 4 == 0.
+__device__ __forceinline__ void rows_dense(const float* A, int K, const float* W, int ldw,
+                                           const float* __restrict__ bias, int n_real, int n_pad, int act,
+                                           float* out, int wave, int lane) {
+  for (int o0 = wave * 4; o0 < n_pad; o0 += 4 * kRowsWaves) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int kc = 0; kc < K; kc += 4) {
+      float av[4];
+      float4 wv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = A[(kc + i) * 64 + lane];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wv[q] = *reinterpret_cast<const float4*>(W + (int64_t)(o0 + q) * ldw + kc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[q] = fmaf(av[0], wv[q].x, acc[q]);
+        acc[q] = fmaf(av[1], wv[q].y, acc[q]);
+        acc[q] = fmaf(av[2], wv[q].z, acc[q]);
+        acc[q] = fmaf(av[3], wv[q].w, acc[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = o0 + q;
+      if (o < n_pad) out[o * 64 + lane] = o < n_real ? act_apply(acc[q] + bias[o], act) : 0.f;
+    }
+  }
+}
+
+// Layer-1 output of F_1 target s for this wave's FS feature columns (lane = row).
+template <int FS>
+__device__ __forceinline__ void rows_h1(const RowsFwdArgs& a, const float* lds, int s, int fo, int lane,
+                                        float (&h)[FS]) {
+  const int* li = reinterpret_cast<const int*>(lds);
+#pragma unroll
+  for (int f = 0; f < FS; ++f) h[f] = 0.f;
+  const int tf0 = li[a.o_l1tgt + s];
+  for (int k = 0; k < a.n_terms1; ++k) {
+    const int kind = a.kind1[k], r = a.rel1[k];
+    const float* T = lds + a.o_tab + k * a.n0 * a.f1_pad + fo;
+    const float* dvr = lds + a.o_dv + r * a.n0 * 64 + lane;
+    float cself, cedge_t;  // self coefficient; per-edge factor (GCN: dt, MEAN: 1/cnt)
+    if (kind == XPG_TERM_ROOT) {
+      cself = 1.f;
+      cedge_t = 0.f;
+    } else {
+      const float kt = lds[a.o_kt + (r * a.n1 + tf0) * 64 + lane];
+      if (kind == XPG_TERM_GCN) {
+        const float dt = inv_sqrt_deg(kt);
+        cself = dt * dt;
+        cedge_t = kt >= 0.f ? dt : 0.f;
+      } else {
+        const int sm = li[a.o_l1smul + r * a.n1 + s];
+        const float cnt = kt + static_cast<float>(sm);
+        const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
+        cself = kt >= 0.f ? static_cast<float>(sm) * inv : 0.f;
+        cedge_t = kt >= 0.f ? inv : 0.f;
+      }
+    }
+    {
+      float v[FS];
+      ld_fs<FS>(T + tf0 * a.f1_pad, v);
+#pragma unroll
+      for (int f = 0; f < FS; ++f) h[f] = fmaf(cself, v[f], h[f]);
+    }
+    if (kind == XPG_TERM_ROOT) continue;
+    const int* pp = li + a.o_l1ptr + r * (a.n1 + 1);
+    const int e0 = pp[s], e1 = pp[s + 1];
+    // GCN edge factor dv_u * dt; MEAN: [u kept] / cnt = min(dv_u * BIG, 1) * inv (dv > 0 iff kept)
+    const float gmul = kind == XPG_TERM_GCN ? cedge_t : 0.f;
+    const float mmul = kind == XPG_TERM_GCN ? 0.f : cedge_t;
+    for (int wb = e0; wb < e1; wb += 64) {
+      const int ne = min(64, e1 - wb);
+      const int vsrc = li[a.o_l1f0 + wb + min(lane, ne - 1)];
+      for (int i0 = 0; i0 < ne; i0 += 4) {
+        int u[4];
+        float d[4], v[4][FS];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) u[q] = rdl(vsrc, min(i0 + q, ne - 1));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] = dvr[u[q] * 64];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ld_fs<FS>(T + u[q] * a.f1_pad, v[q]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float valid = static_cast<float>(i0 + q < ne);
+          const float c = valid * fmaf(d[q], gmul, fminf(d[q] * 1e30f, 1.f) * mmul);
+#pragma unroll
+          for (int f = 0; f < FS; ++f) h[f] = fmaf(c, v[q][f], h[f]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < FS; ++f) {
+    const int fg = fo + f;
+    h[f] = fg < a.f1_out ? act_apply(h[f] + a.bias1[fg], a.act1) : 0.f;
+  }
+}
+
+template <int FS>
+__global__ __launch_bounds__(1024) void k_rows_forward(const RowsFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  int* li = reinterpret_cast<int*>(lds);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t row0 = (int64_t)blockIdx.x * 64, row = row0 + lane;
+  const int nrow = static_cast<int>(a.rows - row0 < 64 ? a.rows - row0 : 64);
+#ifdef XPG_WLM_STAMPS
+  uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stamp_last = __builtin_amdgcn_s_memtime();
+#endif
+  {  // LDS image: layer-1 tables, CSR arrays, layer-2 weights, (staged) mask rows
+    const int n4 = a.n0 * a.f1_pad / 4;
+    for (int k = 0; k < a.n_terms1; ++k) {
+      const float4* src = reinterpret_cast<const float4*>(a.tab1[k]);
+      float4* dst = reinterpret_cast<float4*>(lds + a.o_tab + k * a.n0 * a.f1_pad);
+      for (int i = tid; i < n4; i += 1024) dst[i] = src[i];
+    }
+    auto cp = [&](int off, const int32_t* src, int n) {
+      for (int i = tid; i < n; i += 1024) li[off + i] = src[i];
+    };
+    cp(a.o_dptr, a.deg_ptr, a.n_rel * (a.n0 + 1));
+    cp(a.o_f0n, a.f0_node, a.n0);
+    cp(a.o_dsrc, a.deg_src, a.n_deg_edges);
+    cp(a.o_l1ptr, a.l1_ptr, a.n_rel * (a.n1 + 1));
+    cp(a.o_l1f0, a.l1_f0, a.n1_edges);
+    cp(a.o_l1smul, a.l1_smul, a.n_rel * a.n1);
+    cp(a.o_l1tgt, a.l1_tgt_f0, a.n1);
+    if (a.n_layers == 2) {
+      cp(a.o_l2ptr, a.l2_ptr, a.n_rel * (a.n2 + 1));
+      cp(a.o_l2src, a.l2_src, a.n2_edges);
+      cp(a.o_l2f0, a.l2_f0, a.n2_edges);
+      cp(a.o_l2smul, a.l2_smul, a.n_rel * a.n2);
+      cp(a.o_l2tgt, a.l2_tgt_f0, a.n2);
+      cp(a.o_l2prev, a.l2_tgt_prev, a.n2);
+      if (a.w2_lds) {
+        const int n = a.f2_pad * a.n_terms2 * a.f1_pad / 4;
+        for (int i = tid; i < n; i += 1024)
+          reinterpret_cast<float4*>(lds + a.o_w2)[i] = reinterpret_cast<const float4*>(a.w2)[i];
+      }
+    }
+    for (int i = 0; i < a.n_head; ++i) {
+      if (a.o_hw[i] < 0) continue;
+      const int n = a.H[i].n_pad * a.H[i].k_pad / 4;
+      for (int e = tid; e < n; e += 1024)
+        reinterpret_cast<float4*>(lds + a.o_hw[i])[e] = reinterpret_cast<const float4*>(a.H[i].weight)[e];
+    }
+    if (a.stage_bits) {
+      uint32_t* mb = reinterpret_cast<uint32_t*>(lds + a.o_mb);
+      for (int e = tid; e < 64 * a.words; e += 1024) {
+        const int r = e / a.words, w = e - r * a.words;
+        mb[r * a.mb_pitch + w] = r < nrow ? a.bits[(row0 + r) * a.words + w] : 0u;
+      }
+    }
+  }
+  __syncthreads();
+  XPG_STAMP(0)
+  const uint32_t* mb = reinterpret_cast<const uint32_t*>(lds + a.o_mb);
+  const int64_t rrow = row < a.rows ? row : row0;  // clamped row for unstaged bit reads
+  {  // per (relation, F_0 node) and row: dv = 1/sqrt(1 + kept in-degree) for kept nodes, else 0;
+     // kt = kept in-degree (or -1 when masked) for the F_1 targets (the first n1 F_0 nodes)
+    const int Q = a.n_rel * a.n0;
+    // split the flat (relation, node) range so every wave gets about the same number of edges
+    // plus nodes: first q with ptr(q) + q >= target, by binary search over the LDS ptr array
+    auto flat_ptr = [&](int q) {  // start offset of flat node q (ptr arrays hold absolute offsets)
+      const int r = q / a.n0, p = q - r * a.n0;
+      return li[a.o_dptr + r * (a.n0 + 1) + p];
+    };
+    auto split = [&](int w) {
+      if (w == 0) return 0;
+      if (w == kRowsWaves) return Q;
+      const int64_t target = ((int64_t)(a.n_deg_edges + Q) * w) / kRowsWaves;
+      int lo = 0, hi = Q;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)flat_ptr(mid) + mid < target) lo = mid + 1;
+        else hi = mid;
+      }
+      return lo;
+    };
+    const int q_lo = split(wave), q_hi = split(wave + 1);
+    for (int qb = q_lo; qb < q_hi; qb += 64) {
+      const int nq = min(64, q_hi - qb);
+      const int ql = qb + min(lane, nq - 1);
+      const int rl = ql / a.n0, pl = ql - rl * a.n0;
+      const int vp0 = li[a.o_dptr + rl * (a.n0 + 1) + pl], vp1 = li[a.o_dptr + rl * (a.n0 + 1) + pl + 1];
+      const int vnd = li[a.o_f0n + pl];
+      uint64_t kept = 0;  // bit j: node qb + j is kept in this lane's row
+      for (int j0 = 0; j0 < nq; j0 += 8) {
+        uint32_t wv[8];
+        int nd[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          nd[q] = rdl(vnd, min(j0 + q, nq - 1));
+          wv[q] = row_word(a, mb, rrow, lane, nd[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          kept |= static_cast<uint64_t>(((wv[q] >> (nd[q] & 31)) & 1u) & static_cast<uint32_t>(j0 + q < nq))
+                  << (j0 + q);
+      }
+      auto finish = [&](int j, int c) {
+        const int qq = qb + j, r = qq / a.n0, p = qq - r * a.n0;
+        const bool kp = (kept >> j) & 1ull;
+        const float kin = kp ? static_cast<float>(c) : -1.f;
+        lds[a.o_dv + qq * 64 + lane] = kp ? inv_sqrt_deg(kin) : 0.f;
+        if (p < a.n1) lds[a.o_kt + (r * a.n1 + p) * 64 + lane] = kin;
+      };
+      const int E_lo = rdl(vp0, 0), E_hi = rdl(vp1, nq - 1);
+      int j = 0, a0 = rdl(vp0, 0), a1 = rdl(vp1, 0), c = 0;
+      for (int wb = E_lo; wb < E_hi; wb += 64) {
+        const int ne = min(64, E_hi - wb);
+        const int vsrc = li[a.o_dsrc + wb + min(lane, ne - 1)];
+        uint64_t kb = 0;  // bit i: edge wb + i's source kept in this lane's row
+        for (int i0 = 0; i0 < ne; i0 += 8) {
+          uint32_t wv[8];
+          int sv[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            sv[q] = rdl(vsrc, min(i0 + q, ne - 1));
+            wv[q] = row_word(a, mb, rrow, lane, sv[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            kb |= static_cast<uint64_t>(((wv[q] >> (sv[q] & 31)) & 1u) & static_cast<uint32_t>(i0 + q < ne))
+                  << (i0 + q);
+        }
+        while (j < nq) {  // hand the window's kept edges to the nodes whose segments overlap it
+          const int lo = max(a0, wb) - wb, hi = min(a1, wb + ne) - wb;
+          if (hi > lo) {
+            const uint64_t seg = (hi - lo >= 64 ? ~0ull : ((1ull << (hi - lo)) - 1ull)) << lo;
+            c += __popcll(kb & seg);
+          }
+          if (a1 > wb + ne) break;  // node continues in the next window
+          finish(j, c);
+          c = 0;
+          ++j;
+          if (j < nq) {
+            a0 = rdl(vp0, j);
+            a1 = rdl(vp1, j);
+          }
+        }
+      }
+      for (; j < nq; ++j) {  // nodes without (remaining) edges
+        finish(j, c);
+        c = 0;
+      }
+    }
+  }
+  XPG_STAMP(1)
+  __syncthreads();
+  XPG_STAMP(2)
+  float* h0 = lds + a.o_h0;
+  float* h1b = lds + a.o_h1;
+  const int fo = wave * FS;
+  for (int t = 0; t < a.n_last; ++t) {
+    int cur_w;
+    float h[FS];
+    if (a.n_layers == 1) {
+      rows_h1<FS>(a, lds, t, fo, lane, h);
+#pragma unroll
+      for (int f = 0; f < FS; ++f) h0[(fo + f) * 64 + lane] = h[f];
+      cur_w = a.f1_pad;
+      XPG_STAMP(3)
+      __syncthreads();
+      XPG_STAMP(4)
+    } else {
+      float* A2 = lds + a.o_a2;
+      const int tf0 = li[a.o_l2tgt + t], tp = li[a.o_l2prev + t];
+      for (int k = 0; k < a.n_terms2; ++k) {
+        const int kind = a.kind2[k], r = a.rel2[k];
+        const float* dvr = lds + a.o_dv + r * a.n0 * 64 + lane;
+        float acc[FS];
+#pragma unroll
+        for (int f = 0; f < FS; ++f) acc[f] = 0.f;
+        float cself, cedge_t;
+        int sm = 1;
+        if (kind == XPG_TERM_ROOT) {
+          cself = 1.f;
+          cedge_t = 0.f;
+        } else {
+          const float kt = lds[a.o_kt + (r * a.n1 + tf0) * 64 + lane];
+          if (kind == XPG_TERM_GCN) {
+            const float dt = inv_sqrt_deg(kt);
+            cself = dt * dt;
+            cedge_t = kt >= 0.f ? dt : 0.f;
+          } else {
+            sm = li[a.o_l2smul + r * a.n2 + t];
+            const float cnt = kt + static_cast<float>(sm);
+            const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
+            cself = kt >= 0.f ? static_cast<float>(sm) * inv : 0.f;
+            cedge_t = kt >= 0.f ? inv : 0.f;
+          }
+        }
+        if (sm > 0) {
+          rows_h1<FS>(a, lds, tp, fo, lane, h);
+#pragma unroll
+          for (int f = 0; f < FS; ++f) acc[f] = fmaf(cself, h[f], acc[f]);
+        }
+        if (kind != XPG_TERM_ROOT) {
+          const int e0 = li[a.o_l2ptr + r * (a.n2 + 1) + t], e1 = li[a.o_l2ptr + r * (a.n2 + 1) + t + 1];
+          for (int e = e0; e < e1; ++e) {
+            const int s1 = li[a.o_l2src + e], s0 = li[a.o_l2f0 + e];
+            const float d = dvr[s0 * 64];
+            const float c = kind == XPG_TERM_GCN ? d * cedge_t : (d > 0.f ? cedge_t : 0.f);
+            rows_h1<FS>(a, lds, s1, fo, lane, h);
+#pragma unroll
+            for (int f = 0; f < FS; ++f) acc[f] = fmaf(c, h[f], acc[f]);
+          }
+        }
+#pragma unroll
+        for (int f = 0; f < FS; ++f) A2[(k * a.f1_pad + fo + f) * 64 + lane] = acc[f];
+      }
+      XPG_STAMP(3)
+      __syncthreads();  // A2 complete over all waves' feature columns
+      XPG_STAMP(4)
+      const int K2 = a.n_terms2 * a.f1_pad;
+      if (a.w2_lds) rows_dense(A2, K2, lds + a.o_w2, K2, a.bias2, a.f2_out, a.f2_pad, a.act2, h0, wave, lane);
+      else rows_dense(A2, K2, a.w2, K2, a.bias2, a.f2_out, a.f2_pad, a.act2, h0, wave, lane);
+      cur_w = a.f2_pad;
+      __syncthreads();
+    }
+    XPG_STAMP(5)
+    const float* cur = h0;
+    float* nxt = h1b;
+    for (int i = 0; i < a.n_head; ++i) {
+      const FusedHead& hd = a.H[i];
+      if (a.o_hw[i] >= 0)
+        rows_dense(cur, cur_w, lds + a.o_hw[i], hd.k_pad, hd.bias, hd.n_real, hd.n_pad, hd.act, nxt, wave, lane);
+      else
+        rows_dense(cur, cur_w, hd.weight, hd.k_pad, hd.bias, hd.n_real, hd.n_pad, hd.act, nxt, wave, lane);
+      __syncthreads();
+      const float* tmp = cur;
+      cur = nxt;
+      nxt = const_cast<float*>(tmp);
+      cur_w = hd.n_pad;
+    }
+    if (wave == 0 && lane < nrow) a.y[row * a.n_last + t] = cur[a.out_col * 64 + lane];
+    __syncthreads();
+    XPG_STAMP(6)
+  }
+#ifdef XPG_WLM_STAMPS
+  if (blockIdx.x == 0 && (tid == 0 || tid == 1023)) {
+    for (int q = 0; q < 8; ++q) g_wlm_stamps[tid == 0 ? 0 : 1][q] = stamp_acc[q];
+  }
+#endif
+}
+
 // ------------------------------------------------------------------------------------ surrogate
 // train_model (wlm.py:132-278) in three stages:
 //  1. k_wlm_stats  (grid, block per Adam step): per-step constants that do not depend on w —
@@ -762,19 +1203,7 @@ __global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict_
   }
 }
 
-#ifdef XPG_WLM_STAMPS  // diagnostic build only (tools/wlm_probe.cpp): per-phase cycle counts
-#define XPG_STAMP(k)                                                       \
-  {                                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                     \
-    const uint64_t now_ = __builtin_amdgcn_s_memtime();                    \
-    stamp_acc[k] += now_ - stamp_last;                                     \
-    stamp_last = now_;                                                     \
-    __builtin_amdgcn_sched_barrier(0);                                     \
-  }
-__device__ uint64_t g_wlm_stamps[2][8];
-#else
-#define XPG_STAMP(k)
-#endif
+
 
 constexpr int kTabPitch = 17;  // 16 entries + 1 pad (bank spread across tables)
 constexpr int kStage = 10;     // staged words per thread per buffer (buffer <= 10K words)
@@ -1721,7 +2150,7 @@ int launch_agg(const AggArgs& a, hipStream_t st) {
 
 // Fused single-launch forward when the plan fits (returns 1 when it does not apply).
 int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
-  // opt-in while the per-row latency chains make it slower than the multi-kernel path at c2
+  // opt-in (XPG_FORWARD=fused): per-row latency chains make it slower than k_rows_forward
   const char* env = getenv("XPG_FORWARD");
   if (!env || std::strcmp(env, "fused") != 0) return 1;
   if (p->n_layers > kFusedMaxLayers || p->n_head > kFusedMaxHead) return 1;
@@ -1828,12 +2257,157 @@ int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t r
   return 1;
 }
 
+// Lanes-=-rows fused forward for 1- and 2-layer plans (returns 1 when it does not apply).
+int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
+  if (p->n_layers < 1 || p->n_layers > 2 || p->n_head > kFusedMaxHead) return 1;
+  RowsFwdArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.rows = rows;
+  a.bits = bits;
+  a.y = y;
+  a.words = words_of(p->cols);
+  a.n0 = p->n0;
+  a.n_rel = p->n_rel;
+  a.n_layers = p->n_layers;
+  a.out_col = p->out_col;
+  a.f0_node = p->f0_node;
+  a.deg_ptr = p->deg_ptr;
+  a.deg_src = p->deg_src;
+  a.n_deg_edges = static_cast<int>(p->n_deg_edges);
+  const xpg_layer_desc& l1 = p->layers[0];
+  if (l1.n_terms < 1 || l1.n_terms > XPG_MAX_TERMS || p->n_deg_edges < 0 || l1.n_edges < 0) return 1;
+  a.n1 = l1.n_tgt;
+  a.n1_edges = l1.n_edges;
+  a.n_terms1 = l1.n_terms;
+  a.act1 = l1.act;
+  a.f1_out = l1.f_out;
+  a.f1_pad = l1.f_out_pad;
+  a.l1_ptr = l1.agg_ptr;
+  a.l1_f0 = l1.agg_f0;
+  a.l1_smul = l1.self_mult;
+  a.l1_tgt_f0 = l1.tgt_f0;
+  a.bias1 = l1.bias;
+  for (int k = 0; k < l1.n_terms; ++k) {
+    if (!l1.terms[k].table) return 1;
+    a.kind1[k] = l1.terms[k].kind;
+    a.rel1[k] = l1.terms[k].rel;
+    a.tab1[k] = l1.terms[k].table;
+  }
+  const int fs = a.f1_pad / kRowsWaves;
+  if (a.f1_pad % kRowsWaves || (fs != 2 && fs != 4 && fs != 8)) return 1;
+  int cur_w = a.f1_pad;
+  a.n_last = a.n1;
+  int64_t k2 = 0;
+  if (p->n_layers == 2) {
+    const xpg_layer_desc& l2 = p->layers[1];
+    if (l2.n_terms < 1 || l2.n_terms > XPG_MAX_TERMS || l2.f_in_pad != a.f1_pad || !l2.weight || l2.n_edges < 0)
+      return 1;
+    a.n2 = l2.n_tgt;
+    a.n2_edges = l2.n_edges;
+    a.n_terms2 = l2.n_terms;
+    a.act2 = l2.act;
+    a.f2_out = l2.f_out;
+    a.f2_pad = l2.f_out_pad;
+    a.l2_ptr = l2.agg_ptr;
+    a.l2_src = l2.agg_src;
+    a.l2_f0 = l2.agg_f0;
+    a.l2_smul = l2.self_mult;
+    a.l2_tgt_f0 = l2.tgt_f0;
+    a.l2_tgt_prev = l2.tgt_prev;
+    a.w2 = l2.weight;
+    a.bias2 = l2.bias;
+    for (int k = 0; k < l2.n_terms; ++k) {
+      a.kind2[k] = l2.terms[k].kind;
+      a.rel2[k] = l2.terms[k].rel;
+    }
+    a.n_last = a.n2;
+    cur_w = a.f2_pad;
+    k2 = (int64_t)l2.n_terms * a.f1_pad;
+  }
+  int h0w = cur_w, h1w = 0;
+  a.n_head = p->n_head;
+  for (int i = 0; i < p->n_head; ++i) {
+    const xpg_head_desc& hd = p->head[i];
+    if (hd.k_pad != cur_w || hd.k_pad % 4) return 1;
+    a.H[i].k_pad = hd.k_pad;
+    a.H[i].n_real = hd.n_real;
+    a.H[i].n_pad = hd.n_pad;
+    a.H[i].act = hd.act;
+    a.H[i].weight = hd.weight;
+    a.H[i].bias = hd.bias;
+    if (i % 2 == 0) h1w = std::max(h1w, hd.n_pad);
+    else h0w = std::max(h0w, hd.n_pad);
+    cur_w = hd.n_pad;
+  }
+  if (p->out_col < 0 || p->out_col >= cur_w) return 1;
+  int64_t off = 0;
+  auto take = [&](int64_t n) {
+    const int64_t o = off;
+    off += (n + 3) & ~int64_t(3);
+    return static_cast<int>(o);
+  };
+  a.o_tab = take((int64_t)a.n_terms1 * a.n0 * a.f1_pad);
+  a.o_dv = take((int64_t)a.n_rel * a.n0 * 64);
+  a.o_kt = take((int64_t)a.n_rel * a.n1 * 64);
+  a.o_a2 = take(k2 * 64);
+  a.o_h0 = take((int64_t)h0w * 64);
+  a.o_h1 = take((int64_t)std::max(h1w, 1) * 64);
+  a.o_dptr = take((int64_t)a.n_rel * (a.n0 + 1));
+  a.o_f0n = take(a.n0);
+  a.o_dsrc = take(std::max<int64_t>(1, p->n_deg_edges));
+  a.o_l1ptr = take((int64_t)a.n_rel * (a.n1 + 1));
+  a.o_l1f0 = take(std::max(1, a.n1_edges));
+  a.o_l1smul = take((int64_t)a.n_rel * a.n1);
+  a.o_l1tgt = take(a.n1);
+  a.o_l2ptr = take((int64_t)a.n_rel * (a.n2 + 1));
+  a.o_l2src = take(std::max(1, a.n2_edges));
+  a.o_l2f0 = take(std::max(1, a.n2_edges));
+  a.o_l2smul = take((int64_t)a.n_rel * a.n2);
+  a.o_l2tgt = take(a.n2);
+  a.o_l2prev = take(a.n2);
+  const int64_t cap = 160 * 1024 / 4 - 256;
+  if (off > cap) return 1;
+  a.mb_pitch = a.words | 1;
+  a.stage_bits = off + 64 * (int64_t)a.mb_pitch <= cap ? 1 : 0;
+  if (a.stage_bits) a.o_mb = take(64 * (int64_t)a.mb_pitch);
+  a.w2_lds = 0;
+  if (p->n_layers == 2 && off + (int64_t)a.f2_pad * k2 <= cap) {
+    a.w2_lds = 1;
+    a.o_w2 = take((int64_t)a.f2_pad * k2);
+  }
+  for (int i = 0; i < kFusedMaxHead; ++i) a.o_hw[i] = -1;
+  for (int i = 0; i < p->n_head; ++i) {
+    const int64_t n = (int64_t)p->head[i].n_pad * p->head[i].k_pad;
+    if (off + n <= cap) a.o_hw[i] = take(n);
+  }
+  const size_t lds = sizeof(float) * (size_t)off;
+  const dim3 grid(static_cast<unsigned>(cdiv(rows, 64)));
+#define XPG_ROWS(F)                                                                                     \
+  if (fs == F) {                                                                                        \
+    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_forward<F>),                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));      \
+    hipLaunchKernelGGL(k_rows_forward<F>, grid, dim3(64 * kRowsWaves), lds, st, a);                      \
+    XPG_LAUNCHED();                                                                                     \
+    return XPG_OK;                                                                                      \
+  }
+  XPG_ROWS(2) XPG_ROWS(4) XPG_ROWS(8)
+#undef XPG_ROWS
+  return 1;
+}
+
 }  // namespace
 
 // ==================================================================================== C-ABI
 extern "C" {
 
 int xpg_abi_version(void) { return XPG_ABI_VERSION; }
+
+#ifdef XPG_WLM_STAMPS  // diagnostic build only: per-phase cycle stamps of the last stamped launch
+int xpg_debug_stamps(uint64_t* out) {
+  XPG_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wlm_stamps), sizeof(uint64_t) * 16));
+  return XPG_OK;
+}
+#endif
 
 const char* xpg_last_error(void) { return g_err.c_str(); }
 
@@ -1922,8 +2496,18 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   XPG_REQ(p->n_rel >= 1 && p->n0 >= 1 && p->cols > 0, "masked_forward: bad plan sizes");
   if (rows == 0) return XPG_OK;
   hipStream_t st = S(stream);
-  rc = try_fused_forward(p, bits, rows, y, st);
-  if (rc != 1) return rc;
+  {
+    const char* env = getenv("XPG_FORWARD");
+    const bool multi = env && std::strcmp(env, "unfused") == 0;
+    const bool wave_rows = env && std::strcmp(env, "fused") == 0;
+    if (wave_rows) {
+      rc = try_fused_forward(p, bits, rows, y, st);
+      if (rc != 1) return rc;
+    } else if (!multi) {
+      rc = try_rows_forward(p, bits, rows, y, st);
+      if (rc != 1) return rc;
+    }
+  }
   char* ws = static_cast<char*>(workspace);
   float* kin = reinterpret_cast<float*>(ws + L.kin);
   const int words = words_of(p->cols);

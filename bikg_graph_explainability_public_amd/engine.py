@@ -210,6 +210,7 @@ class ForwardPlan:
             ld.f_out = conv.f_out
             ld.f_out_pad = f_out_pad
             ld.n_tgt = n_t
+            ld.n_edges = int(arr["layers"][li]["agg_src"].size)
             ld.f_in_pad = 0 if li == 0 else prev_pad
             ld.tgt_prev = self._i32(np.arange(n_t)).data_ptr()  # F_l is a prefix of F_{l-1}
             ld.tgt_f0 = self._i32(arr["pos"][0][fr[lvl]]).data_ptr()
@@ -262,7 +263,8 @@ class ForwardPlan:
         self.n_out = fr[L].size
         self.desc = ForwardPlanDesc(
             cols=S, n_rel=self.n_rel, n0=n0, f0_node=self._f0_node.data_ptr(),
-            deg_ptr=self._deg_ptr.data_ptr(), deg_src=self._deg_src.data_ptr(), n_layers=L,
+            deg_ptr=self._deg_ptr.data_ptr(), deg_src=self._deg_src.data_ptr(),
+            n_deg_edges=int(arr["deg_src"].size), n_layers=L,
             layers=self._layers, n_head=len(program.head), head=self._head,
             out_col=program.out_col)
         self._ws = None

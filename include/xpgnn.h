@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 3
+#define XPG_ABI_VERSION 4
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -102,6 +102,7 @@ typedef struct xpg_layer_desc {
   int32_t f_out;           /* real output width                                        */
   int32_t f_out_pad;       /* padded output width, % 32 == 0, <= 256                   */
   int32_t n_tgt;           /* |F_l|                                                    */
+  int32_t n_edges;         /* agg_src / agg_f0 length (all relations)                  */
   const int32_t* tgt_prev; /* [n_tgt] position of each target inside F_{l-1}          */
   const int32_t* tgt_f0;   /* [n_tgt] position of each target inside F_0               */
   const int32_t* agg_ptr;  /* [n_rel * (n_tgt + 1)] in-edges per target, self-loops out */
@@ -126,6 +127,7 @@ typedef struct xpg_forward_plan {
   const int32_t* f0_node;  /* [n0] subgraph node id of each F_0 position              */
   const int32_t* deg_ptr;  /* [n_rel * (n0 + 1)] in-edges of F_0 nodes, self-loops out */
   const int32_t* deg_src;  /* subgraph node ids                                        */
+  int64_t n_deg_edges;     /* deg_src length (all relations)                           */
   int32_t n_layers;
   const xpg_layer_desc* layers;   /* host array [n_layers]                             */
   int32_t n_head;

@@ -29,10 +29,11 @@ def _eng():
     return engine
 
 
-@pytest.fixture(params=["fused", "unfused"])
+@pytest.fixture(params=["rows", "fused", "unfused"])
 def fwd_path(request, monkeypatch):
-    """xpg_masked_forward has two HIP paths: the multi-kernel path (default) and the
-    single-launch fused kernel for plans that fit in LDS (XPG_FORWARD=fused)."""
+    """xpg_masked_forward has three HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
+    (default), the wave-per-row fused kernel (XPG_FORWARD=fused) and the multi-kernel path
+    (XPG_FORWARD=unfused, also the fallback for plans the fused kernels do not take)."""
     monkeypatch.setenv("XPG_FORWARD", request.param)
     return request.param
 
@@ -168,6 +169,38 @@ def test_masked_forward_vs_oracle_fp64(fwd_path):
         ref = oracle.masked_query_outputs(spec, sub_x, rel_ei, m, sub_ind)
         got = plan.forward(e.pack_masks(torch.as_tensor(m).to(DEV)))[:, 0].cpu().numpy()
         np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind,dims,fc", [("gcn", [16, 32], [32, 1]),
+                                           ("sage", [16, 32], [32, 8, 1]),
+                                           ("gcn", [16, 128, 64], [64, 1]),
+                                           ("sage", [16, 64, 32], [32, 16, 1]),
+                                           ("gcn", [16, 32, 32, 32], [32, 1])])
+def test_masked_forward_synthetic_archs(kind, dims, fc, fwd_path):
+    """1-, 2- and 3-layer GCN / SAGE stacks of several widths (each fused kernel's template
+    variants and the fallback) on a random graph with self-loops and duplicate edges, vs the
+    fp64 oracle."""
+    from golden_utils import oracle_spec
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    e = _eng()
+    g = torch.Generator().manual_seed(17)
+    S, E = 300, 1500
+    x = torch.randn((S, dims[0]), generator=g)
+    ei = torch.randint(0, S, (2, E), generator=g)
+    ei[:, :20] = ei[0, :20]  # self-loops
+    ei[:, 20:40] = ei[:, 40:60]  # duplicate edges
+    torch.manual_seed(3)
+    arch = ConvStack(kind, dims, fc).eval()
+    q = int(ei[1, 100])
+    plan = pipeline.build_plan(arch.to(DEV), x.to(DEV), ei.to(DEV), [q])
+    spec = oracle_spec({"arch_spec": {"kind": kind, "dims": dims, "fc": fc}},
+                       {k: v.detach().cpu().numpy() for k, v in arch.state_dict().items()})
+    rng = np.random.default_rng(5)
+    m = rng.random((130, S)) < rng.random((130, 1))
+    ref = oracle.masked_query_outputs(spec, x.numpy(), {None: ei.numpy()}, m, q)
+    got = plan.forward(e.pack_masks(torch.as_tensor(m).to(DEV)))[:, 0].cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)
 
 
 def test_generic_path_matches_engine():
@@ -371,11 +404,11 @@ def test_c2_scale_forward_properties(fwd_path):
     np.testing.assert_allclose(y_off, ref_off[0], atol=1e-5)
     k = e.shap_kernel(bits, S)
     assert torch.isfinite(k).all() and (k >= 0).all()
-    if fwd_path == "fused":  # the two HIP paths agree on every row
+    if fwd_path != "unfused":  # the fused paths agree with the multi-kernel path on every row
         import os
         os.environ["XPG_FORWARD"] = "unfused"
         try:
             y3 = plan.forward(bits)[:, 0]
         finally:
-            os.environ["XPG_FORWARD"] = "fused"
+            os.environ["XPG_FORWARD"] = fwd_path
         torch.testing.assert_close(y3, y, rtol=0, atol=2e-6)

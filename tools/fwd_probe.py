@@ -1,0 +1,47 @@
+"""Diagnostic (not part of the product): per-phase cycle stamps of k_rows_forward and event
+timings of the three forward paths on the c2 bench workload.
+
+    XPG_LIB=tools/libxpgnn_stamps.so python tools/fwd_probe.py
+(libxpgnn_stamps.so = xpgnn.hip built with -DXPG_WLM_STAMPS; see scripts/gpu_check.sh)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from bikg_graph_explainability_public_amd import _lib, engine  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    args = bench.parse()
+    arch, sub_feat, sub_ei, q, plan = bench.build_workload(args, dev)
+    S = plan.cols
+    bits = engine.sample_shapley(7, 12800, S, dev)
+    names = ["prologue", "degree", "sync", "L2 agg (h1)", "sync", "dense L2", "head+y"]
+    for path in ("rows", "fused", "unfused"):
+        os.environ["XPG_FORWARD"] = path
+        for _ in range(3):
+            plan.forward(bits)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(20):
+            plan.forward(bits)
+        b.record()
+        torch.cuda.synchronize()
+        print(f"{path:8s} forward 12800 rows: {a.elapsed_time(b) / 20 * 1e3:8.1f} us", flush=True)
+        if path == "rows" and hasattr(lib, "xpg_debug_stamps"):
+            st = (ctypes.c_uint64 * 16)()
+            lib.xpg_debug_stamps(st)
+            v = np.array(list(st), dtype=np.float64).reshape(2, 8)
+            for i, n in enumerate(names):
+                print(f"   {n:14s} wave0 {v[0, i]:9.0f}  wave3 {v[1, i]:9.0f} cycles")
+
+
+if __name__ == "__main__":
+    main()
