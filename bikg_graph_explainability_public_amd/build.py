@@ -23,8 +23,10 @@ def build(force=False, verbose=True):
     if not force and os.path.exists(OUT) and \
             all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-o", OUT + ".tmp", SRC]
+    # -fno-slp-vectorize: SLP pairs independent per-row/column chains into packed fp32 ops and
+    # keeps both halves live (the grid surrogate kernels spill; no kernel here gains from it)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC",
+           "-shared", "-Wall", "-o", OUT + ".tmp", SRC]
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -102,25 +102,53 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
   return c;
 }
 
-__global__ void k_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
-                          int words, uint32_t* __restrict__ bits) {
+// grid (ceil(quads / 256), min(rows, 65535)); thread = one 16-byte quad (4 words) of a row.
+// ALIGN: 4 -> rows start 16-B aligned (words % 4 == 0): one dwordx4 store; 2 -> 8-B aligned
+// (words even): two dwordx2 stores; 1 -> four dword stores.  counts != nullptr: the row's
+// popcount is accumulated (one atomic per block and row; the caller zeroes counts first), which
+// spares KernelSHAP a second pass over the bits (kernels.py:144 row sums).
+template <int ALIGN>
+__global__ __launch_bounds__(256) void k_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
+                                                 int words, uint32_t* __restrict__ bits,
+                                                 int32_t* __restrict__ counts) {
+  __shared__ int red[4];
   const int quads = (words + 3) / 4;
-  int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (idx >= rows * quads) return;
-  int64_t r = idx / quads;
-  int q = static_cast<int>(idx - r * quads);
-  uint64_t gr = (uint64_t)(row_offset + r);
-  uint4 o = philox4x32_10(make_uint4((uint32_t)q, (uint32_t)gr, (uint32_t)(gr >> 32), 0x58504721u),
-                          (uint32_t)seed, (uint32_t)(seed >> 32));
-  uint32_t v[4] = {o.x, o.y, o.z, o.w};
+  const int q = blockIdx.x * 256 + threadIdx.x;
   const int tail = static_cast<int>(cols & 31);
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    int pc = 0;
+    if (q < quads) {
+      const uint64_t gr = static_cast<uint64_t>(row_offset + r);
+      const uint4 o = philox4x32_10(make_uint4(static_cast<uint32_t>(q), static_cast<uint32_t>(gr),
+                                               static_cast<uint32_t>(gr >> 32), 0x58504721u),
+                                    static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+      uint32_t v[4] = {o.x, o.y, o.z, o.w};
+      const int w0 = q * 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int w = q * 4 + j;
-    if (w < words) {
-      uint32_t x = v[j];
-      if (w == words - 1 && tail) x &= (1u << tail) - 1u;
-      bits[r * words + w] = x;
+      for (int j = 0; j < 4; ++j) {
+        if (w0 + j >= words) v[j] = 0u;
+        else if (w0 + j == words - 1 && tail) v[j] &= (1u << tail) - 1u;
+        pc += __popc(v[j]);
+      }
+      uint32_t* dst = bits + r * words + w0;
+      if (ALIGN == 4 && w0 + 4 <= words) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(v[0], v[1], v[2], v[3]);
+      } else if (ALIGN == 2 && w0 + 4 <= words) {
+        reinterpret_cast<uint2*>(dst)[0] = make_uint2(v[0], v[1]);
+        reinterpret_cast<uint2*>(dst)[1] = make_uint2(v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (w0 + j < words) dst[j] = v[j];
+      }
+    }
+    if (counts) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) pc += __shfl_xor(pc, off, 64);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = pc;
+      __syncthreads();
+      if (threadIdx.x == 0) atomicAdd(counts + r, red[0] + red[1] + red[2] + red[3]);
+      __syncthreads();
     }
   }
 }
@@ -144,8 +172,16 @@ __global__ void k_popcount(const uint32_t* __restrict__ bits, int64_t rows, int 
   int64_t r = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
   if (r >= rows) return;
   const uint32_t* row = bits + r * words;
-  int c = 0;
-  for (int w = lane; w < words; w += 64) c += __popc(row[w]);
+  int c = 0, c1 = 0, c2 = 0, c3 = 0;
+  int w = lane;
+  for (; w + 192 < words; w += 256) {  // 4 independent loads in flight per lane
+    c += __popc(row[w]);
+    c1 += __popc(row[w + 64]);
+    c2 += __popc(row[w + 128]);
+    c3 += __popc(row[w + 192]);
+  }
+  for (; w < words; w += 64) c += __popc(row[w]);
+  c += c1 + c2 + c3;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
   if (lane == 0) counts[r] = c;
@@ -1841,39 +1877,74 @@ __global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hi
 
 // -------------------------------------------------------------- surrogate, many-column (grid) fit
 // For S beyond the single-workgroup fit (graph_prediction on large graphs, regime (ii)) each
-// Adam step is three grid launches over 2048-column chunks (64 mask words), streaming the step's
-// B x S mask bits from HBM twice (HBM-bound: 2 * B * S / 8 bytes per step):
-//   k_gw_p     per chunk: nibble tables of w in LDS; 64-row tiles staged through LDS, lanes =
-//              rows (one table per lane group: conflict-free); partial p_j per workgroup
+// Adam step is three grid launches over 2048-column chunks (64 mask words).  Both bit-streaming
+// kernels read the step's B x S mask bits once, coalesced (lane = mask word, 32 rows per load
+// round, 32 loads in flight per lane), so a step costs 2 * B * S / 8 bytes of HBM reads plus the
+// Adam state:
+//   k_gw_p     p_j = (M_b w)_j per chunk: nibble tables of w in LDS laid out [nibble pos][value]
+//              [word] (lane = word: every lane its own bank), then a butterfly transpose-reduce
+//              of the lane's 32 row partials over the wave; partial p per (chunk, row)
 //   k_gw_g     p_j = sum of the partials, g_j = 2 k_j (p_j - ybar) / (B sum k), the loss term
-//   k_gw_grad  per chunk: nibble tables of g in LDS; the tile's bits are transposed by wave
-//              ballots (lane b keeps column b's 64-row mask); (M_b^T g)_i by lookups, then the
-//              Adam update of the chunk's columns and the chunk's sum |w| for the loss
-constexpr int kGwWords = 64;                // mask words per chunk (2048 columns)
-constexpr int kGwThreads = 512;             // 8 waves x 8 words
-constexpr int kGwTilePitch = kGwWords + 1;  // odd pitch: lanes = rows hit distinct banks
+//   k_gw_grad  (M_b^T g)_c per chunk: each lane transposes its 32 x 32 bit block in registers
+//              (5 butterfly stages), then one lookup per nibble into 4-row tables of g; the four
+//              waves' column sums meet in LDS; Adam update of the chunk's columns and sum |w|
+constexpr int kGwWords = 64;    // mask words per chunk (2048 columns)
+constexpr int kGpWaves = 8;     // k_gw_p: waves per workgroup
+constexpr int kGgWaves = 4;     // k_gw_grad: waves per workgroup
 
-__device__ __forceinline__ void gw_load_tile(const uint32_t* __restrict__ bits, int64_t words, int64_t row0,
-                                             int nrows, int64_t w0, int nw, uint32_t* tile) {
-  const int tid = threadIdx.x;
-  const int r = tid >> 3, seg = (tid & 7) * 8;  // 64 rows x 8 segments of 8 words
+// Sum of v[0..31] over the wave's 64 lanes for every i: after the call lanes 2i and 2i + 1 hold
+// sum_lanes v[i] in v[0] (5 halving exchange stages + a final pair add).
+__device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lane) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int wd = seg + q;
-    uint32_t x = 0u;
-    if (r < nrows && wd < nw) x = bits[(row0 + r) * words + w0 + wd];
-    tile[r * kGwTilePitch + wd] = x;
+  for (int st = 0; st < 5; ++st) {
+    const int half = 16 >> st;            // values kept after this stage
+    const int xm = 32 >> st;              // partner lane distance
+    const bool hi = (lane & xm) != 0;
+#pragma unroll
+    for (int k = 0; k < half; ++k) {
+      float lo_v = v[k], hi_v = v[k + half];
+      asm volatile("" : "+v"(lo_v), "+v"(hi_v));  // opaque: keeps the selects on values, not indices
+      const float keep = hi ? hi_v : lo_v;
+      const float send = hi ? lo_v : hi_v;
+      float r = keep + __shfl_xor(send, xm);
+      asm volatile("" : "+v"(r));
+      v[k] = r;
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1);
+}
+
+// In-register 32 x 32 bit transpose: in a[i] bit b = M[i][b], out a[b] bit i = M[i][b].
+__device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
+#pragma unroll
+  for (int j = 16, s = 0; j != 0; j >>= 1, ++s) {
+    const uint32_t m = s == 0 ? 0x0000FFFFu : s == 1 ? 0x00FF00FFu : s == 2 ? 0x0F0F0F0Fu
+                     : s == 3 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+    for (int k = 0; k < 32; k = (k + j + 1) & ~j) {
+      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
+      a[k + j] ^= t;
+      a[k] ^= t << j;
+    }
   }
 }
 
-__global__ __launch_bounds__(kGwThreads) void k_gw_p(const uint32_t* __restrict__ bits, int64_t rows,
-                                                     int64_t cols, int64_t words, int batch, int64_t t,
-                                                     const float* __restrict__ wg, float* __restrict__ p_part) {
-  extern __shared__ __attribute__((aligned(16))) float gsm[];
-  float* T = gsm;                                                        // [64*8][17]
-  uint32_t* tile = reinterpret_cast<uint32_t*>(T + kGwWords * 8 * kTabPitch);  // [64][65]
-  float* red = reinterpret_cast<float*>(tile + 64 * kGwTilePitch);      // [8][64]
-  float* pacc = red + 8 * 64;                                            // [batch]
+// x[i] = word `wd` of row row0 + i for i < nr, else 0.  row0 / nr are wave-uniform, so the row
+// test is a scalar branch and all loads are in flight together (no per-lane exec masking);
+// callers mask lanes past the chunk.
+__device__ __forceinline__ void gw_load32(const uint32_t* __restrict__ bits, int64_t words, int64_t row0, int nr,
+                                          uint32_t wd, uint32_t (&x)[32]) {
+  typedef const __attribute__((address_space(1))) uint32_t gu32;
+  gu32* base = (gu32*)(bits + row0 * words);
+#pragma unroll
+  for (int i = 0; i < 32; ++i) x[i] = i < nr ? base[(int64_t)i * words + wd] : 0u;  // uniform branch
+}
+
+// grid (n_chunks, n_fits), kGpWaves * 64 threads; p_part [n_fits][n_chunks][batch]
+__global__ __launch_bounds__(kGpWaves * 64) void k_gw_p(const uint32_t* __restrict__ bits, int64_t rows,
+                                                       int64_t cols, int64_t words, int batch, int64_t t,
+                                                       const float* __restrict__ wg, float* __restrict__ p_part) {
+  __shared__ float T[8 * 16 * kGwWords];  // T[(q * 16 + v) * 64 + j]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t f = blockIdx.y;
   bits += f * rows * words;
@@ -1881,52 +1952,58 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_p(const uint32_t* __restrict_
   p_part += (f * gridDim.x + blockIdx.x) * (int64_t)batch;
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
-  const int64_t n_chunks = (words + kGwWords - 1) / kGwWords;
-  for (int j = tid; j < batch; j += kGwThreads) pacc[j] = 0.f;
-  for (int64_t ck = blockIdx.x; ck < n_chunks; ck += gridDim.x) {
-    const int64_t w0 = ck * kGwWords;
-    const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
-    __syncthreads();  // previous chunk's readers of T are done
-    for (int e = tid; e < kGwWords * 8 * 16; e += kGwThreads) {  // table (word, nibble) entry v
-      const int tb = e >> 4, v = e & 15;
-      const int64_t c = (w0 + (tb >> 3)) * 32 + (tb & 7) * 4;
-      float s = 0.f;
+  const int64_t w0 = (int64_t)blockIdx.x * kGwWords;
+  const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
+  const uint32_t lmask = lane < nw ? ~0u : 0u;
+  const uint32_t wd = static_cast<uint32_t>(w0 + (lane < nw ? lane : 0));
+  const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform row blocks
+  uint32_t x[32];
+  if (wv * 32 < B) gw_load32(bits, words, r0 + wv * 32, min(32, B - wv * 32), wd, x);  // in flight
+  for (int task = tid; task < 8 * kGwWords; task += kGpWaves * 64) {  // during the table build:
+    const int j = task & (kGwWords - 1), q = task >> 6;                // (word, nibble position)
+    const int64_t c = (w0 + j) * 32 + 4 * q;
+    float a[4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) s += ((v >> b) & 1) && c + b < cols ? wg[c + b] : 0.f;
-      T[tb * kTabPitch + v] = s;
-    }
-    for (int rb = 0; rb * 64 < B; ++rb) {
-      const int nr = min(64, B - rb * 64);
-      __syncthreads();  // tile free
-      gw_load_tile(bits, words, r0 + rb * 64, nr, w0, nw, tile);
-      __syncthreads();
-      float s = 0.f;
-      const uint32_t* row = tile + lane * kGwTilePitch;
-#pragma unroll 2
-      for (int q = 0; q < 8; ++q) {
-        const int wd = wave * 8 + q;
-        s += nib8(T + (wd * 8) * kTabPitch, row[wd]);  // words >= nw are zero -> entry 0 = 0
-      }
-      red[wave * 64 + lane] = s;
-      __syncthreads();
-      if (tid < 64 && tid < nr) {
-        float p = 0.f;
+    for (int b = 0; b < 4; ++b) a[b] = c + b < cols ? wg[c + b] : 0.f;
+    float* Tq = T + q * 16 * kGwWords + j;  // entry v at Tq[v * 64]: lanes = words, no conflicts
 #pragma unroll
-        for (int w = 0; w < 8; ++w) p += red[w * 64 + tid];
-        pacc[rb * 64 + tid] += p;
-      }
-    }
+    for (int v = 0; v < 16; ++v)
+      Tq[v * kGwWords] = ((v & 1) ? a[0] : 0.f) + ((v & 2) ? a[1] : 0.f) + ((v & 4) ? a[2] : 0.f) +
+                         ((v & 8) ? a[3] : 0.f);
   }
   __syncthreads();
-  for (int j = tid; j < B; j += kGwThreads) p_part[j] = pacc[j];
+  const float* Tl = T + lane;
+#pragma unroll 1
+  for (int rb = wv; rb * 32 < B; rb += kGpWaves) {
+    const int nr = min(32, B - rb * 32);
+    uint32_t xn[32];  // next block's words, in flight during this block's lookups
+    const int rbn = rb + kGpWaves;
+    if (rbn * 32 < B) gw_load32(bits, words, r0 + rbn * 32, min(32, B - rbn * 32), wd, xn);
+    float c[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint32_t xi = i < nr ? (x[i] & lmask) : 0u;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += Tl[(q * 16 + ((xi >> (4 * q)) & 15u)) * kGwWords];
+      c[i] = s;
+    }
+    const float tot = wave_transpose_reduce32(c, lane);
+    const int i = (lane >> 1) & 31;
+    if (!(lane & 1) && i < nr) p_part[rb * 32 + i] = tot;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) x[k] = xn[k];
+  }
 }
 
-__global__ __launch_bounds__(256) void k_gw_g(const float* __restrict__ p_part, int n_wg, int64_t rows,
-                                              int batch, int64_t t, const double* __restrict__ kern,
-                                              const WlmStep* __restrict__ stp, int64_t steps,
-                                              float* __restrict__ g, float* __restrict__ p_hist,
-                                              double* __restrict__ tk_part) {
-  __shared__ double red[16];
+// grid (ceil(batch / 64), n_fits), 1024 threads: 16 waves split the partials of 64 rows
+__global__ __launch_bounds__(1024) void k_gw_g(const float* __restrict__ p_part, int n_wg, int64_t rows,
+                                               int batch, int64_t t, const double* __restrict__ kern,
+                                               const WlmStep* __restrict__ stp, int64_t steps,
+                                               float* __restrict__ g, float* __restrict__ p_hist,
+                                               double* __restrict__ tk_part) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t f = blockIdx.y;
   p_part += f * n_wg * (int64_t)batch;
   kern += f * rows;
@@ -1935,27 +2012,39 @@ __global__ __launch_bounds__(256) void k_gw_g(const float* __restrict__ p_part, 
   const WlmStep sc = stp[f * steps + t];
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int j = blockIdx.x * 64 + lane;
+  float p = 0.f;
+  if (j < B) {
+#pragma unroll 8
+    for (int w = wave; w < n_wg; w += 16) p += p_part[(int64_t)w * batch + j];
+  }
+  red[wave][lane] = p;
+  __syncthreads();
+  if (wave != 0) return;
+  p = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) p += red[w][lane];
   double tk = 0.0;
   if (j < B) {
-    float p = 0.f;
-    for (int w = 0; w < n_wg; ++w) p += p_part[(int64_t)w * batch + j];
     const double kj = kern[r0 + j];
     const double d = static_cast<double>(p) - sc.ybar;
     g[j] = static_cast<float>(kj * (2.0 / (static_cast<double>(B) * sc.ksum)) * d);
     p_hist[r0 + j] = p;
     tk = kj * d * d;
   }
-  const double T = block_sum_d(tk, red);
-  if (threadIdx.x == 0) tk_part[(f * steps + t) * gridDim.x + blockIdx.x] = T;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tk += __shfl_xor(tk, o);
+  if (lane == 0) tk_part[(f * steps + t) * gridDim.x + blockIdx.x] = tk;
 }
 
-__global__ __launch_bounds__(kGwThreads) void k_gw_grad(const uint32_t* __restrict__ bits, int64_t rows,
-                                                        int64_t cols, int64_t words, int batch, int64_t t,
-                                                        const float* __restrict__ g, const WlmStep* __restrict__ stp,
-                                                        int64_t steps, xpg_wlm_params P, float* __restrict__ wg,
-                                                        float* __restrict__ mg, float* __restrict__ vg,
-                                                        double* __restrict__ aw_part) {
+// grid (n_chunks, n_fits), kGgWaves * 64 threads, dynamic LDS 16 * (ceil(batch/32) * 8 | 1) + 2080
+// floats (rounded to 4)
+__global__ __launch_bounds__(kGgWaves * 64) void k_gw_grad(const uint32_t* __restrict__ bits, int64_t rows,
+                                                          int64_t cols, int64_t words, int batch, int64_t t,
+                                                          const float* __restrict__ g, const WlmStep* __restrict__ stp,
+                                                          int64_t steps, xpg_wlm_params P, float* __restrict__ wg,
+                                                          float* __restrict__ mg, float* __restrict__ vg,
+                                                          double* __restrict__ aw_part) {
   extern __shared__ __attribute__((aligned(16))) float gsm[];
   __shared__ double red[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1968,67 +2057,76 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_grad(const uint32_t* __restri
   const WlmStep sc = stp[f * steps + t];
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
-  const int ngrp = ((batch + 63) / 64) * 16;  // every 4-row group of every 64-row tile
-  float* G = gsm;                                                        // [ngrp][17]
-  uint32_t* tile = reinterpret_cast<uint32_t*>(G + ((ngrp * kTabPitch + 3) & ~3));  // [64][65]
-  for (int e = tid; e < ngrp * 16; e += kGwThreads) {
-    const int grp = e >> 4, v = e & 15;
-    float s = 0.f;
+  const int ngrp = ((B + 31) / 32) * 8;  // 4-row groups of whole 32-row blocks (tail groups 0)
+  const int64_t w0 = (int64_t)blockIdx.x * kGwWords;
+  const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
+  const uint32_t lmask = lane < nw ? ~0u : 0u;
+  const uint32_t wd = static_cast<uint32_t>(w0 + (lane < nw ? lane : 0));
+  const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform row blocks
+  uint32_t x[32];
+  if (wv * 32 < B) gw_load32(bits, words, r0 + wv * 32, min(32, B - wv * 32), wd, x);  // in flight
+  const int gp = ngrp | 1;                     // odd pitch: the 16 entries of a group on 16 banks
+  float* G = gsm;                              // G[v * gp + group]
+  float* colsum = gsm + ((16 * gp + 3) & ~3);  // [32 bit][65]: column (word j, bit b) at b * 65 + j
+  for (int grp = tid; grp < ngrp; grp += kGgWaves * 64) {  // thread = 4-row group: subset sums
+    float a[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int j = 4 * grp + b;
-      s += ((v >> b) & 1) && j < B ? g[j] : 0.f;
+    for (int b = 0; b < 4; ++b) a[b] = 4 * grp + b < B ? g[4 * grp + b] : 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      G[v * gp + grp] = ((v & 1) ? a[0] : 0.f) + ((v & 2) ? a[1] : 0.f) + ((v & 4) ? a[2] : 0.f) +
+                        ((v & 8) ? a[3] : 0.f);
+  }
+  for (int e = tid; e < 32 * 65; e += kGgWaves * 64) colsum[e] = 0.f;
+  __syncthreads();
+  float acc[32];
+#pragma unroll
+  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+#pragma unroll 1
+  for (int rb = wv; rb * 32 < B; rb += kGgWaves) {
+    const int nr = min(32, B - rb * 32);
+    uint32_t xn[32];  // next block's words, in flight during this block's transpose + lookups
+    const int rbn = rb + kGgWaves;
+    if (rbn * 32 < B) gw_load32(bits, words, r0 + rbn * 32, min(32, B - rbn * 32), wd, xn);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) x[i] = i < nr ? (x[i] & lmask) : 0u;
+    transpose32(x);  // x[b] = column 32 * word + b over the block's 32 rows
+    const float* Gb = G + rb * 8;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      float s = 0.f;
+#pragma unroll
+      for (int n = 0; n < 8; ++n) s += Gb[((x[b] >> (4 * n)) & 15u) * gp + n];  // rows past B: bits 0
+      acc[b] += s;
     }
-    G[grp * kTabPitch + v] = s;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) x[k] = xn[k];
+  }
+  for (int w = 0; w < kGgWaves; ++w) {  // waves add in a fixed order: deterministic sums
+    if (wave == w) {
+#pragma unroll
+      for (int b = 0; b < 32; ++b) colsum[b * 65 + lane] += acc[b];
+    }
+    __syncthreads();
   }
   const float l1s = P.l1_lambda / static_cast<float>(cols);
-  const int64_t n_chunks = (words + kGwWords - 1) / kGwWords;
   double aw = 0.0;
-  for (int64_t ck = blockIdx.x; ck < n_chunks; ck += gridDim.x) {
-    const int64_t w0 = ck * kGwWords;
-    const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int rb = 0; rb * 64 < B; ++rb) {
-      const int nr = min(64, B - rb * 64);
-      __syncthreads();  // tile free (and G complete on the first pass)
-      gw_load_tile(bits, words, r0 + rb * 64, nr, w0, nw, tile);
-      __syncthreads();
-      const uint32_t* row = tile + lane * kGwTilePitch;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int wd = wave * 8 + 2 * q;
-        const uint32_t x0 = row[wd], x1 = row[wd + 1];
-        uint32_t lo = 0u, hi = 0u;  // this lane's column: 64-row mask (rows rb*64 + 0..63)
-#pragma unroll
-        for (int b = 0; b < 32; ++b) {
-          const uint64_t m0 = __ballot((x0 >> b) & 1u);
-          const uint64_t m1 = __ballot((x1 >> b) & 1u);
-          const uint64_t m = (lane & 31) == b ? ((lane >> 5) ? m1 : m0) : 0ull;
-          lo |= static_cast<uint32_t>(m);
-          hi |= static_cast<uint32_t>(m >> 32);
-        }
-        const float* gt = G + (rb * 16) * kTabPitch;
-        acc[q] += nib8(gt, lo) + nib8(gt + 8 * kTabPitch, hi);
-      }
-    }
-    // Adam on this chunk's columns: lane < 32 -> word wd, lane >= 32 -> word wd + 1
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t c = (w0 + wave * 8 + 2 * q + (lane >> 5)) * 32 + (lane & 31);
-      if (c < cols) {
-        float w = wg[c], m = mg[c], v = vg[c];
-        aw += fabs(static_cast<double>(w));
-        const float sgn = w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f);
-        float gr = fmaf(l1s, sgn, acc[q]);
-        gr = fmaf(P.weight_decay, w, gr);
-        m = fmaf(1.f - P.beta1, gr - m, m);
-        v = fmaf(1.f - P.beta2, gr * gr, v * P.beta2);
-        const float denom = sqrtf(v) / sc.bc2_sqrt + P.eps;
-        w = w - sc.step_size * (m / denom);
-        wg[c] = w;
-        mg[c] = m;
-        vg[c] = v;
-      }
+  for (int e = tid; e < 32 * kGwWords; e += kGgWaves * 64) {
+    const int64_t c = w0 * 32 + e;
+    if (c < cols) {
+      const float gsum = colsum[(e & 31) * 65 + (e >> 5)];
+      float w = wg[c], m = mg[c], v = vg[c];
+      aw += fabs(static_cast<double>(w));
+      const float sgn = w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f);
+      float gr = fmaf(l1s, sgn, gsum);
+      gr = fmaf(P.weight_decay, w, gr);
+      m = fmaf(1.f - P.beta1, gr - m, m);
+      v = fmaf(1.f - P.beta2, gr * gr, v * P.beta2);
+      const float denom = sqrtf(v) / sc.bc2_sqrt + P.eps;
+      w = w - sc.step_size * (m / denom);
+      wg[c] = w;
+      mg[c] = m;
+      vg[c] = v;
     }
   }
   const double A = block_sum_d(aw, red);
@@ -2395,6 +2493,23 @@ int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t ro
   return 1;
 }
 
+int launch_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits, int32_t* counts,
+                   hipStream_t st) {
+  const int words = words_of(cols);
+  const int quads = (words + 3) / 4;
+  if (rows == 0) return XPG_OK;
+  XPG_REQ(quads <= (1 << 30), "shapley: row too long");
+  const dim3 grid(static_cast<unsigned>(cdiv(quads, 256)), static_cast<unsigned>(std::min<int64_t>(rows, 65535)));
+  if (words % 4 == 0)
+    hipLaunchKernelGGL(k_shapley<4>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts);
+  else if (words % 2 == 0)
+    hipLaunchKernelGGL(k_shapley<2>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts);
+  else
+    hipLaunchKernelGGL(k_shapley<1>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
 }  // namespace
 
 // ==================================================================================== C-ABI
@@ -2432,12 +2547,15 @@ int xpg_unpack_masks(const uint32_t* bits, int64_t rows, int64_t cols, uint8_t* 
 
 int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits, xpg_stream_t stream) {
   XPG_REQ(rows >= 0 && cols > 0 && row_offset >= 0, "shapley: bad shape");
-  const int words = words_of(cols);
-  const int64_t n = rows * ((words + 3) / 4);
-  if (n == 0) return XPG_OK;
-  hipLaunchKernelGGL(k_shapley, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, S(stream), seed, row_offset, rows, cols, words, bits);
-  XPG_LAUNCHED();
-  return XPG_OK;
+  return launch_shapley(seed, row_offset, rows, cols, bits, nullptr, S(stream));
+}
+
+int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits,
+                              int32_t* counts, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 0 && row_offset >= 0 && counts, "shapley: bad shape");
+  if (rows == 0) return XPG_OK;
+  XPG_HIP(hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)rows, S(stream)));
+  return launch_shapley(seed, row_offset, rows, cols, bits, counts, S(stream));
 }
 
 int xpg_edge_keep(const uint32_t* bits, int64_t rows, int64_t cols, const int32_t* src, const int32_t* dst,
@@ -2639,11 +2757,10 @@ static int wlm_layout_grid(int64_t n_fits, int64_t rows, int64_t cols, int64_t b
   XPG_REQ(batch <= 8192, "wlm_fit: batch > 8192 rows is not supported by the many-column fit");
   L->grid = true;
   L->stage = false;
-  L->n_wg = static_cast<int>(std::min<int64_t>(cdiv(words, kGwWords), 512));
-  L->n_tk = static_cast<int>(cdiv(batch, 256));
-  L->lds_p = sizeof(float) * (size_t)(kGwWords * 8 * kTabPitch + 64 * kGwTilePitch + 8 * 64 + batch);
-  L->lds_g = sizeof(float) * (size_t)((((batch + 63) / 64) * 16 * kTabPitch + 3) & ~3) +
-             sizeof(uint32_t) * 64 * kGwTilePitch;
+  L->n_wg = static_cast<int>(cdiv(words, kGwWords));
+  L->n_tk = static_cast<int>(cdiv(batch, 64));
+  L->lds_p = 0;  // static
+  L->lds_g = sizeof(float) * (size_t)(((16 * ((((batch + 31) / 32) * 8) | 1) + 3) & ~3) + 32 * 65);
   const size_t F = static_cast<size_t>(n_fits);
   size_t off = 0;
   L->steps_off = off;
@@ -2753,18 +2870,16 @@ static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib, P,
                      step0, stp);
   XPG_LAUNCHED();
-  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gw_p), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(L.lds_p)));
   XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gw_grad),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_g)));
   const dim3 gw(static_cast<unsigned>(L.n_wg), nf);
   for (int64_t t = 0; t < steps; ++t) {
-    hipLaunchKernelGGL(k_gw_p, gw, dim3(kGwThreads), L.lds_p, st, bits, rows, cols, words, ib, t, w, p_part);
+    hipLaunchKernelGGL(k_gw_p, gw, dim3(kGpWaves * 64), 0, st, bits, rows, cols, words, ib, t, w, p_part);
     XPG_LAUNCHED();
-    hipLaunchKernelGGL(k_gw_g, dim3(static_cast<unsigned>(L.n_tk), nf), dim3(256), 0, st, p_part, L.n_wg, rows, ib,
+    hipLaunchKernelGGL(k_gw_g, dim3(static_cast<unsigned>(L.n_tk), nf), dim3(1024), 0, st, p_part, L.n_wg, rows, ib,
                        t, kernel, stp, steps, g, p_hist, tk_part);
     XPG_LAUNCHED();
-    hipLaunchKernelGGL(k_gw_grad, gw, dim3(kGwThreads), L.lds_g, st, bits, rows, cols, words, ib, t, g, stp, steps,
+    hipLaunchKernelGGL(k_gw_grad, gw, dim3(kGgWaves * 64), L.lds_g, st, bits, rows, cols, words, ib, t, g, stp, steps,
                        P, w, adam_m, adam_v, aw_part);
     XPG_LAUNCHED();
   }

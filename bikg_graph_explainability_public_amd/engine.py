@@ -49,12 +49,21 @@ def unpack_masks(bits: torch.Tensor, cols: int) -> torch.Tensor:
     return out.view(torch.bool)
 
 
-def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0):
-    """Device Shapley masks (masks.py:231-260 distribution: iid Bernoulli(1/2) bits)."""
+def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0,
+                   with_counts: bool = False):
+    """Device Shapley masks (masks.py:231-260 distribution: iid Bernoulli(1/2) bits).
+
+    with_counts=True also returns the per-row popcounts (int32 [rows]) accumulated while
+    sampling, for `shap_kernel(..., counts=...)`."""
     bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=device)
-    call("xpg_sample_shapley", ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), row_offset, rows,
-         cols, ptr(bits), _lib.stream_of(torch.device(device)))
-    return bits
+    st = _lib.stream_of(torch.device(device))
+    seed_c = ctypes.c_uint64(int(seed) & (2 ** 64 - 1))
+    if not with_counts:
+        call("xpg_sample_shapley", seed_c, row_offset, rows, cols, ptr(bits), st)
+        return bits
+    counts = torch.empty(rows, dtype=torch.int32, device=device)
+    call("xpg_sample_shapley_counts", seed_c, row_offset, rows, cols, ptr(bits), ptr(counts), st)
+    return bits, counts
 
 
 def edge_keep(bits, cols, src, dst):
@@ -70,14 +79,21 @@ def edge_keep(bits, cols, src, dst):
 
 
 # ----------------------------------------------------------------------------- KernelSHAP
-def shap_kernel(bits: torch.Tensor, cols: int) -> torch.Tensor:
-    """Kernel.compute (kernels.py:115-174) on device: fp64 [rows]."""
+def shap_kernel(bits: torch.Tensor, cols: int, counts: torch.Tensor = None) -> torch.Tensor:
+    """Kernel.compute (kernels.py:115-174) on device: fp64 [rows].  `counts` (row popcounts from
+    `sample_shapley(..., with_counts=True)`) skips the popcount pass over the bits."""
     _lib.require_device(bits, "bits")
     rows = bits.shape[0]
-    counts = torch.empty(rows, dtype=torch.int32, device=bits.device)
     out = torch.empty(rows, dtype=torch.float64, device=bits.device)
     st = _lib.stream_of(bits.device)
-    call("xpg_popcount_rows", ptr(bits), rows, cols, ptr(counts), st)
+    if counts is None:
+        counts = torch.empty(rows, dtype=torch.int32, device=bits.device)
+        call("xpg_popcount_rows", ptr(bits), rows, cols, ptr(counts), st)
+    else:
+        _lib.require_device(counts, "counts")
+        if counts.dtype != torch.int32 or counts.numel() != rows:
+            raise ValueError("counts must be int32 [rows]")
+        counts = counts.contiguous()
     call("xpg_shap_kernel", ptr(counts), rows, cols, ptr(out), st)
     return out
 

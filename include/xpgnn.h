@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 4
+#define XPG_ABI_VERSION 5
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -62,6 +62,10 @@ int xpg_unpack_masks(const uint32_t* bits, int64_t rows, int64_t cols, uint8_t* 
 /* Shapley masks, P(bit) = 1/2, counter-based Philox4x32-10 keyed by (seed, global row). */
 int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
                        uint32_t* bits, xpg_stream_t stream);
+/* Same bits, plus counts[r] = popcount of row r (the KernelSHAP coalition sizes, kernels.py:144),
+ * accumulated while sampling so KernelSHAP needs no second pass over the bits. */
+int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
+                              uint32_t* bits, int32_t* counts, xpg_stream_t stream);
 
 /* ---------------------------------------------------------------- perturbation */
 /* keep[b*n_edges + e] = bit(b, src[e]) & bit(b, dst[e])   (data.py:420-449) */

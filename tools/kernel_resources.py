@@ -4,7 +4,7 @@ import subprocess
 import sys
 
 src = sys.argv[1] if len(sys.argv) > 1 else "bikg_graph_explainability_public_amd/csrc/xpgnn.hip"
-out = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", "-o", "/tmp/_kr.o",
+out = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-c", "-o", "/tmp/_kr.o",
                       __import__("os").path.abspath(src), "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True,
                      cwd="/tmp").stderr
 cur, rows = None, {}
