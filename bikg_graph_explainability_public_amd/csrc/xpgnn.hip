@@ -62,6 +62,21 @@ __device__ __forceinline__ float act_apply(float x, int act) {
   }
 }
 
+// In-register 32 x 32 bit transpose: in a[i] bit b = M[i][b], out a[b] bit i = M[i][b].
+__device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
+#pragma unroll
+  for (int j = 16, s = 0; j != 0; j >>= 1, ++s) {
+    const uint32_t m = s == 0 ? 0x0000FFFFu : s == 1 ? 0x00FF00FFu : s == 2 ? 0x0F0F0F0Fu
+                     : s == 3 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+    for (int k = 0; k < 32; k = (k + j + 1) & ~j) {
+      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
+      a[k + j] ^= t;
+      a[k] ^= t << j;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------ masks
 __global__ void k_pack(const uint8_t* __restrict__ m, int64_t rows, int64_t cols, int words,
                        uint32_t* __restrict__ bits) {
@@ -1151,6 +1166,553 @@ __global__ __launch_bounds__(1024) void k_rows_forward(const RowsFwdArgs a) {
 #endif
 }
 
+// ------------------------------------------------------------------------------ wide forward
+// Masked forward for LARGE frontiers (the full-graph regime: every node a target, SURVEY.md §8d
+// (ii)), 2-layer plans, 32 mask rows ("samples") per pass:
+//   k_wide_bits    row bits -> node-major words mT[node] (bit s = sample s), 32 x 32 register
+//                  transposes; k_wide_f0 gathers them to F_0 order (mT0)
+//   k_wide_degree  (GCN terms) kept in-degree of every F_0 node for all 32 samples: kinT
+//   k_wide_l1      layer 1 for all 32 samples at once, wave = target: each kept in-edge's table
+//                  row X W^T is read ONCE per 32 samples (features are never masked, data.py:582)
+//                  and scattered into 32 per-sample accumulators with per-sample coefficients
+//   k_wide_last    layer 2 + head, workgroup = (sample, 32 targets): 16-lane groups gather the
+//                  kept h1 rows of their targets (4 rows in flight per group) into an LDS tile,
+//                  v_mfma_f32_32x32x2_f32 against the layer weights, bias/act, the dense head
+//                  on the tile, and the output column.
+// Same arithmetic per target as k_agg / k_dense.
+constexpr int kWideS = 32;  // samples per pass
+
+__global__ __launch_bounds__(256) void k_wide_bits(const uint32_t* __restrict__ bits, int64_t row0, int nr,
+                                                   int words, int64_t cols, uint32_t* __restrict__ mT) {
+  const int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (w >= words) return;
+  uint32_t x[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) x[i] = i < nr ? bits[(row0 + i) * words + w] : 0u;
+  transpose32(x);
+#pragma unroll
+  for (int b = 0; b < 32; ++b) {
+    const int64_t c = w * 32 + b;
+    if (c < cols) mT[c] = x[b];
+  }
+}
+
+__global__ void k_wide_f0(const uint32_t* __restrict__ mT, const int32_t* __restrict__ f0_node, int n0,
+                          uint32_t* __restrict__ mT0) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n0) mT0[p] = mT[f0_node[p]];
+}
+
+// kinT[(r * n0 + p) * 32 + s]: kept in-degree (self-loops out) of F_0 node p under relation r in
+// sample s, -1 when the node is masked out in s.  Thread = (item (r, p), sample s).
+__global__ __launch_bounds__(256) void k_wide_degree(const uint32_t* __restrict__ mT, const uint32_t* __restrict__ mT0,
+                                                     int n0, int n_rel, const int32_t* __restrict__ deg_ptr,
+                                                     const int32_t* __restrict__ deg_src, float* __restrict__ kinT) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t item = gid >> 5;
+  const int sidx = static_cast<int>(gid & 31);
+  if (item >= (int64_t)n_rel * n0) return;
+  const int r = static_cast<int>(item / n0), p = static_cast<int>(item - (int64_t)r * n0);
+  float out = -1.f;
+  if ((mT0[p] >> sidx) & 1u) {
+    const int32_t* pp = deg_ptr + (int64_t)r * (n0 + 1);
+    int c = 0;
+    for (int e = pp[p]; e < pp[p + 1]; ++e) c += (mT[deg_src[e]] >> sidx) & 1u;
+    out = static_cast<float>(c);
+  }
+  kinT[item * 32 + sidx] = out;
+}
+
+struct WideArgs {
+  int64_t row0;  // global index of the block's first mask row (output rows of the last layer)
+  int nr, n0, n_src, n_tgt, n_rel, n_terms, w_row, f_real, act;
+  int agg1;  // the only aggregating (non-ROOT) term, or -1 when there are several
+  int head1;  // the head is one Linear(f_out, 1) (+ act) read at column 0: fused epilogue
+  int dbg;   // diagnostics (XPG_WIDE_DBG): 1 skip dense + head, 2 skip row gathers, 4 head, 8 dense
+  int K, a_ld, f_out, f_out_pad, n_head, out_col, h_ld, o_h0, o_h1, o_e;
+  int o_hw[kFusedMaxHead];
+  const uint32_t* mT0;
+  const float* kinT;
+  const float* src;  // last layer: h1 [32][n_src][w_row]
+  const float* table[XPG_MAX_TERMS];  // layer 1: X W_k^T [n0][w_row]
+  const int32_t* tgt_prev;
+  const int32_t* tgt_f0;
+  const int32_t* agg_ptr;
+  const int32_t* agg_src;
+  const int32_t* agg_f0;
+  const int32_t* self_mult;
+  const float* weight;  // last layer: [f_out_pad][K]
+  const float* bias;
+  int kind[XPG_MAX_TERMS], rel[XPG_MAX_TERMS];
+  FusedHead H[kFusedMaxHead];
+  float* out;  // layer 1: h1 [32][n_tgt][w_row]; last layer: y [rows][n_tgt]
+};
+
+constexpr int kWideCap = 256;  // staged in-edges per target (all terms, one per thread); more: in place
+
+// Sum of coef * source row over the kept in-edges [e0, e1) of one term for sample sidx (4 rows in
+// flight per 16-lane group): STAGED reads (row, F_0 position, keep word) from the LDS stage,
+// otherwise from the CSR in place.  Returns the number of kept edges.
+template <int NFI, bool STAGED>
+__device__ __forceinline__ int wide_gather_rows(const WideArgs& a, int k, int e0, int e1, const int* rowv,
+                                                const int* u0v, const uint32_t* mv, int sidx, int kind, int r,
+                                                float dt, const float* base, int fo, float (&acc)[NFI]) {
+  int cnt = 0;
+  for (int e = e0; e < e1; e += 4) {
+    int row[4], u0[4];
+    uint32_t m[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // indices of 4 edges first (independent loads)
+      const int ee = e + j < e1 ? e + j : e0;
+      row[j] = rowv[ee];
+      u0[j] = u0v[ee];
+      m[j] = STAGED ? mv[ee] : 0u;
+    }
+    if (!STAGED) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] = a.mT0[u0[j]];
+    }
+    float cf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool kept = e + j < e1 && ((m[j] >> sidx) & 1u);
+      cf[j] = !kept ? 0.f : (kind == XPG_TERM_GCN ? dt * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + u0[j]) * 32 + sidx]) : 1.f);
+    }
+    float rr[4][NFI];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int i = 0; i < NFI; ++i) rr[j][i] = 0.f;
+      if (cf[j] != 0.f) {
+        const float* sp = base + (int64_t)row[j] * a.w_row + fo;
+        if (NFI % 4 == 0) {
+#pragma unroll
+          for (int i = 0; i < NFI / 4; ++i) {
+            const float4 v = reinterpret_cast<const float4*>(sp)[i];
+            rr[j][4 * i] = v.x;
+            rr[j][4 * i + 1] = v.y;
+            rr[j][4 * i + 2] = v.z;
+            rr[j][4 * i + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NFI / 2; ++i) {
+            const float2 v = reinterpret_cast<const float2*>(sp)[i];
+            rr[j][2 * i] = v.x;
+            rr[j][2 * i + 1] = v.y;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cnt += cf[j] != 0.f;
+#pragma unroll
+      for (int i = 0; i < NFI; ++i) acc[i] = fmaf(cf[j], rr[j][i], acc[i]);
+    }
+  }
+  return cnt;
+}
+
+// Both samples of a 16-lane group over the staged in-edges [e0, e1) of one term: 16 edges per
+// round are tested lane-parallel, the kept ones of either sample are compacted with ballots and
+// fetched RIF rows at a time (a slot takes sample s0's next kept edge, else s1's).
+template <int NFI, int RIF>
+__device__ __forceinline__ void wide_gather2(const WideArgs& a, int e0, int e1, const int* Esrc, const int* Eu0,
+                                             const uint32_t* Em, int s0, int s1, bool tk0, bool tk1, int kind, int r,
+                                             float dt0, float dt1, const float* base0, const float* base1, int fo,
+                                             int gl, int lb, float (&acc0)[NFI], float (&acc1)[NFI], int& cnt0,
+                                             int& cnt1) {
+  for (int c0 = e0; c0 < e1; c0 += 16) {
+    const int e = c0 + gl;
+    const uint32_t m = e < e1 ? Em[e] : 0u;
+    uint32_t m0 = static_cast<uint32_t>(__ballot(tk0 && ((m >> s0) & 1u)) >> lb) & 0xFFFFu;
+    uint32_t m1 = static_cast<uint32_t>(__ballot(tk1 && ((m >> s1) & 1u)) >> lb) & 0xFFFFu;
+    cnt0 += __popc(m0);
+    cnt1 += __popc(m1);
+    while (m0 | m1) {
+      float rr[RIF][NFI];
+      float c0v[RIF], c1v[RIF];
+#pragma unroll
+      for (int q = 0; q < RIF; ++q) {
+        int j = -1;
+        bool first = false;
+        if (m0) {
+          j = __builtin_ctz(m0);
+          m0 &= m0 - 1u;
+          first = true;
+        } else if (m1) {
+          j = __builtin_ctz(m1);
+          m1 &= m1 - 1u;
+        }
+        c0v[q] = c1v[q] = 0.f;
+#pragma unroll
+        for (int i = 0; i < NFI; ++i) rr[q][i] = 0.f;
+        if (j >= 0) {
+          const int ee = c0 + j;
+          const float* bp = first ? base0 : base1;
+          const float* sp = bp + (int64_t)Esrc[ee] * a.w_row + fo;
+          const int sidx = first ? s0 : s1;
+          const float c = kind == XPG_TERM_GCN
+                              ? (first ? dt0 : dt1) * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + Eu0[ee]) * 32 + sidx])
+                              : 1.f;
+          c0v[q] = first ? c : 0.f;
+          c1v[q] = first ? 0.f : c;
+          if (NFI % 4 == 0) {
+#pragma unroll
+            for (int i = 0; i < NFI / 4; ++i) {
+              const float4 v = reinterpret_cast<const float4*>(sp)[i];
+              rr[q][4 * i] = v.x;
+              rr[q][4 * i + 1] = v.y;
+              rr[q][4 * i + 2] = v.z;
+              rr[q][4 * i + 3] = v.w;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < NFI / 2; ++i) {
+              const float2 v = reinterpret_cast<const float2*>(sp)[i];
+              rr[q][2 * i] = v.x;
+              rr[q][2 * i + 1] = v.y;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < RIF; ++q)
+#pragma unroll
+        for (int i = 0; i < NFI; ++i) {
+          acc0[i] = fmaf(c0v[q], rr[q][i], acc0[i]);
+          acc1[i] = fmaf(c1v[q], rr[q][i], acc1[i]);
+        }
+    }
+  }
+}
+
+// One launch per conv layer of a 2-layer plan, persistent (target += gridDim.x).  Item = one
+// target for all 32 samples of the pass.  Its in-edges of every term (source row, F_0 position,
+// 32-sample keep word) are staged in LDS once; then the 16 lane-groups of 16 lanes own samples
+// g and g + 16 and gather their sample's kept source rows (NFI = w_row / 16 floats per lane,
+// 4 rows in flight per group), in a fixed order per (target, sample): bitwise reproducible.
+//   LAST = false (layer 1): sources are the shared tables X W_k^T (features are never masked,
+//     data.py:582); the sum over terms + bias + act is written to h1[s][t].
+//   LAST = true (layer 2 + head): each term's aggregate fills the sample's row of the A tile
+//     (32 samples x K), v_mfma_f32_32x32x2_f32 against the layer weights (KW > 0: held in
+//     registers, K = 8 KW; else read from L2), bias + act, the dense head on the tile, and the
+//     output column for the 32 samples.
+template <int NFI, bool LAST, int KW>
+__global__ __launch_bounds__(256, LAST ? 2 : (NFI >= 12 ? 2 : 3)) void k_wide_tgt(const WideArgs a) {
+  constexpr int RIF = (LAST && KW > 0) || NFI >= 8 ? 4 : 8;  // rows in flight per 16-lane group
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  float* A = wsm;  // LAST: [32][a_ld]
+  int* Esrc = reinterpret_cast<int*>(wsm + a.o_e);
+  int* Eu0 = Esrc + kWideCap;
+  uint32_t* Em = reinterpret_cast<uint32_t*>(Eu0 + kWideCap);
+  __shared__ int seg[XPG_MAX_TERMS + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = tid >> 4, gl = tid & 15, fo = gl * NFI;
+  const int i32 = lane & 31, h = lane >> 5;
+  float4 wreg[KW > 0 ? KW : 1];
+  if (LAST) {
+    if (KW > 0 && wave * 32 < a.f_out_pad) {
+      const float* wp = a.weight + (int64_t)(wave * 32 + i32) * a.K + 4 * h;
+#pragma unroll
+      for (int kk = 0; kk < (KW > 0 ? KW : 1); ++kk) wreg[kk] = *reinterpret_cast<const float4*>(wp + kk * 8);
+    }
+    for (int li = 0; li < a.n_head; ++li) {  // head weights: once per (persistent) workgroup
+      const FusedHead& hd = a.H[li];
+      for (int e = tid; e < hd.n_real * hd.k_pad; e += 256) wsm[a.o_hw[li] + e] = hd.weight[e];
+    }
+  }
+  // Software pipeline over this workgroup's targets: the next target's CSR ranges and edge
+  // indices are loaded while the current one gathers, its keep words while it computes; the
+  // staged edges are committed to LDS at the top of the next iteration (one edge per thread).
+  int pf_seg[XPG_MAX_TERMS + 1], pf_p0[XPG_MAX_TERMS];
+  int pf_u0 = 0, pf_src = 0, pf_tf0 = 0, pf_tp = 0;
+  uint32_t pf_m = 0u, pf_mv = 0u;
+  auto prefetch_idx = [&](int tn) {
+    int off = 0, e = 0;
+    if (a.agg1 >= 0) {  // one aggregating term (homogeneous GCN / SAGE): one CSR range, no loop
+      const int32_t* pp = a.agg_ptr + (int64_t)a.rel[a.agg1] * (a.n_tgt + 1);
+      const int b0 = pp[tn], b1 = pp[tn + 1];
+#pragma unroll
+      for (int k = 0; k <= XPG_MAX_TERMS; ++k) pf_seg[k] = k <= a.agg1 ? 0 : b1 - b0;
+      off = b1 - b0;
+      e = b0 + tid;
+    } else {
+#pragma unroll
+      for (int k = 0; k < XPG_MAX_TERMS; ++k) {
+        pf_seg[k] = off;
+        pf_p0[k] = 0;
+        if (k < a.n_terms && a.kind[k] != XPG_TERM_ROOT) {
+          const int32_t* pp = a.agg_ptr + (int64_t)a.rel[k] * (a.n_tgt + 1);
+          pf_p0[k] = pp[tn];
+          off += pp[tn + 1] - pf_p0[k];
+        }
+      }
+      pf_seg[XPG_MAX_TERMS] = off;
+#pragma unroll
+      for (int k = 0; k < XPG_MAX_TERMS; ++k)
+        if (k < a.n_terms && a.kind[k] != XPG_TERM_ROOT && tid >= pf_seg[k]) e = pf_p0[k] + (tid - pf_seg[k]);
+    }
+    pf_tf0 = a.tgt_f0[tn];
+    pf_tp = LAST ? a.tgt_prev[tn] : pf_tf0;
+    if (off <= kWideCap && tid < off) {
+      pf_u0 = a.agg_f0[e];
+      pf_src = LAST ? a.agg_src[e] : pf_u0;
+    }
+  };
+  auto prefetch_m = [&]() {
+    pf_mv = a.mT0[pf_tf0];
+    if (pf_seg[XPG_MAX_TERMS] <= kWideCap && tid < pf_seg[XPG_MAX_TERMS]) pf_m = a.mT0[pf_u0];
+  };
+  if (blockIdx.x < a.n_tgt) {
+    prefetch_idx(blockIdx.x);
+    prefetch_m();
+  }
+  for (int t = blockIdx.x; t < a.n_tgt; t += gridDim.x) {
+    const int tn = t + gridDim.x;
+    __syncthreads();  // the previous item's readers of E / A / the head tiles are done
+    const int total = pf_seg[XPG_MAX_TERMS];
+    const bool staged = total <= kWideCap;
+    if (staged && tid < total) {
+      Esrc[tid] = pf_src;
+      Eu0[tid] = pf_u0;
+      Em[tid] = pf_m;
+    }
+    if (tid == 0) {
+#pragma unroll
+      for (int k = 0; k <= XPG_MAX_TERMS; ++k) seg[k] = pf_seg[k];  // term k: [seg[k], seg[k + 1])
+    }
+    const int tf0 = pf_tf0, tp = pf_tp;
+    const uint32_t mv = pf_mv;
+    if (tn < a.n_tgt) prefetch_idx(tn);
+    __syncthreads();
+    // ---- gather: group g owns samples s0 = g and s1 = g + 16
+    {
+      const int s0 = g, s1 = g + 16;
+      const bool v0 = s0 < a.nr, v1 = s1 < a.nr;
+      const bool tk0 = v0 && ((mv >> s0) & 1u), tk1 = v1 && ((mv >> s1) & 1u);
+      float tot0[NFI], tot1[NFI];
+#pragma unroll
+      for (int i = 0; i < NFI; ++i) tot0[i] = tot1[i] = 0.f;
+      for (int k = 0; k < a.n_terms; ++k) {
+        const int kind = a.kind[k], r = a.rel[k];
+        const float* base0 = LAST ? a.src + (int64_t)(v0 ? s0 : 0) * a.n_src * a.w_row : a.table[k];
+        const float* base1 = LAST ? a.src + (int64_t)(v1 ? s1 : 0) * a.n_src * a.w_row : a.table[k];
+        float self0[NFI], self1[NFI];
+        {
+          const float* p0r = base0 + (int64_t)tp * a.w_row + fo;
+          const float* p1r = base1 + (int64_t)tp * a.w_row + fo;
+#pragma unroll
+          for (int i = 0; i < NFI; ++i) {
+            self0[i] = p0r[i];
+            self1[i] = LAST ? p1r[i] : self0[i];
+          }
+        }
+        float acc0[NFI], acc1[NFI];
+        if (kind == XPG_TERM_ROOT) {
+#pragma unroll
+          for (int i = 0; i < NFI; ++i) {
+            acc0[i] = self0[i];
+            acc1[i] = self1[i];
+          }
+        } else {
+          float dt0 = 1.f, dt1 = 1.f;
+          if (kind == XPG_TERM_GCN) {
+            dt0 = inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + s0]);
+            dt1 = inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + s1]);
+          }
+#pragma unroll
+          for (int i = 0; i < NFI; ++i) acc0[i] = acc1[i] = 0.f;
+          int cnt0 = 0, cnt1 = 0;
+          if (a.dbg & 2) {
+          } else if (staged) {
+            wide_gather2<NFI, RIF>(a, seg[k], seg[k + 1], Esrc, Eu0, Em, s0, s1, tk0, tk1, kind, r, dt0, dt1, base0,
+                                   base1, fo, gl, (lane & 48), acc0, acc1, cnt0, cnt1);
+          } else {
+            const int32_t* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+            if (tk0)
+              cnt0 = wide_gather_rows<NFI, false>(a, k, pp[t], pp[t + 1], LAST ? a.agg_src : a.agg_f0, a.agg_f0,
+                                                  nullptr, s0, kind, r, dt0, base0, fo, acc0);
+            if (tk1)
+              cnt1 = wide_gather_rows<NFI, false>(a, k, pp[t], pp[t + 1], LAST ? a.agg_src : a.agg_f0, a.agg_f0,
+                                                  nullptr, s1, kind, r, dt1, base1, fo, acc1);
+          }
+          if (kind == XPG_TERM_GCN) {
+#pragma unroll
+            for (int i = 0; i < NFI; ++i) {
+              acc0[i] = fmaf(dt0 * dt0, self0[i], acc0[i]);
+              acc1[i] = fmaf(dt1 * dt1, self1[i], acc1[i]);
+            }
+          } else {  // MEAN: 0 when the target is masked out in the sample
+            const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+            const float inv0 = tk0 ? 1.f / static_cast<float>(max(cnt0 + sm, 1)) : 0.f;
+            const float inv1 = tk1 ? 1.f / static_cast<float>(max(cnt1 + sm, 1)) : 0.f;
+#pragma unroll
+            for (int i = 0; i < NFI; ++i) {
+              acc0[i] = fmaf(static_cast<float>(sm), self0[i], acc0[i]) * inv0;
+              acc1[i] = fmaf(static_cast<float>(sm), self1[i], acc1[i]) * inv1;
+            }
+          }
+        }
+        if (LAST) {
+#pragma unroll
+          for (int i = 0; i < NFI; ++i) {
+            A[s0 * a.a_ld + k * a.w_row + fo + i] = v0 ? acc0[i] : 0.f;
+            A[s1 * a.a_ld + k * a.w_row + fo + i] = v1 ? acc1[i] : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NFI; ++i) {
+            tot0[i] += acc0[i];
+            tot1[i] += acc1[i];
+          }
+        }
+      }
+      if (!LAST) {
+        float o0[NFI], o1[NFI];
+#pragma unroll
+        for (int i = 0; i < NFI; ++i) {
+          const int f = fo + i;
+          const float bv = f < a.f_real ? a.bias[f] : 0.f;
+          o0[i] = f < a.f_real ? act_apply(tot0[i] + bv, a.act) : 0.f;
+          o1[i] = f < a.f_real ? act_apply(tot1[i] + bv, a.act) : 0.f;
+        }
+        if (v0) {
+          float* o = a.out + ((int64_t)s0 * a.n_tgt + t) * a.w_row + fo;
+#pragma unroll
+          for (int i = 0; i < NFI; ++i) o[i] = o0[i];
+        }
+        if (v1) {
+          float* o = a.out + ((int64_t)s1 * a.n_tgt + t) * a.w_row + fo;
+#pragma unroll
+          for (int i = 0; i < NFI; ++i) o[i] = o1[i];
+        }
+      }
+    }
+    if (tn < a.n_tgt) prefetch_m();
+    if (!LAST || (a.dbg & 1)) continue;
+    __syncthreads();
+    // ---- dense: C[32 samples x f_out_pad] = act(A W^T + b), wave = 32-column blocks
+    float* H0 = wsm + a.o_h0;
+    for (int nb = wave; nb * 32 < a.f_out_pad && !(a.dbg & 8); nb += 4) {
+      f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+      const float* ap = A + i32 * a.a_ld + 4 * h;
+      if (KW > 0) {
+#pragma unroll
+        for (int kk = 0; kk < (KW > 0 ? KW : 1); ++kk) {
+          const float4 av = *reinterpret_cast<const float4*>(ap + kk * 8);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wreg[kk].x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wreg[kk].y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wreg[kk].z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wreg[kk].w, acc, 0, 0, 0);
+        }
+      } else {  // weights streamed from L2, PF float4 loads ahead; two independent MFMA chains
+        constexpr int PF = 8;
+        const float* wp = a.weight + (int64_t)(nb * 32 + i32) * a.K + 4 * h;
+        float4 wb[PF];
+#pragma unroll
+        for (int j = 0; j < PF; ++j)
+          wb[j] = j * 8 < a.K ? *reinterpret_cast<const float4*>(wp + j * 8) : make_float4(0.f, 0.f, 0.f, 0.f);
+        f32x16 acc2;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc2[q] = 0.f;
+        for (int kc0 = 0; kc0 < a.K; kc0 += 8 * PF) {  // K % 16 == 0 (host check)
+#pragma unroll
+          for (int j = 0; j < PF; j += 2) {
+            const int kc = kc0 + 8 * j;
+            if (kc < a.K) {
+              const float4 av = *reinterpret_cast<const float4*>(ap + kc);
+              const float4 av2 = *reinterpret_cast<const float4*>(ap + kc + 8);
+              const float4 wv = wb[j], wv2 = wb[j + 1];
+              if (kc + 8 * PF < a.K) {
+                wb[j] = *reinterpret_cast<const float4*>(wp + kc + 8 * PF);
+                wb[j + 1] = *reinterpret_cast<const float4*>(wp + kc + 8 + 8 * PF);
+              }
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wv.x, acc, 0, 0, 0);
+              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.x, wv2.x, acc2, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wv.y, acc, 0, 0, 0);
+              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.y, wv2.y, acc2, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wv.z, acc, 0, 0, 0);
+              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.z, wv2.z, acc2, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wv.w, acc, 0, 0, 0);
+              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.w, wv2.w, acc2, 0, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
+      }
+      const int col = nb * 32 + i32;
+      const float bv = col < a.f_out ? a.bias[col] : 0.f;
+      if (a.head1) {  // single-logit head: the dot with its weight row, reduced over the block's columns
+        const float hwc = col < a.f_out ? wsm[a.o_hw[0] + col] : 0.f;
+        float part[16];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          part[reg] = col < a.f_out ? act_apply(acc[reg] + bv, a.act) * hwc : 0.f;
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) part[reg] += __shfl_xor(part[reg], o);
+        if (i32 == 0) {  // lanes 0 and 32 hold the 16 sample rows of their half
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) H0[nb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = part[reg];
+        }
+      } else {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          H0[row * a.h_ld + col] = col < a.f_out ? act_apply(acc[reg] + bv, a.act) : 0.f;
+        }
+      }
+    }
+    __syncthreads();
+    if (a.head1) {  // y[s] = act(sum over column blocks + b)
+      if (tid < a.nr) {
+        float v = 0.f;
+        for (int nb = 0; nb * 32 < a.f_out_pad; ++nb) v += H0[nb * 32 + tid];
+        a.out[(a.row0 + tid) * a.n_tgt + t] = act_apply(v + a.H[0].bias[0], a.H[0].act);
+      }
+      continue;
+    }
+    // ---- head on the tile: out[s][n] = act(sum_k cur[s][k] W[n][k] + b[n]) (n < n_real; pad 0)
+    float* cur = H0;
+    float* nxt = wsm + a.o_h1;
+    int cur_w = a.f_out_pad;
+    for (int li = 0; li < a.n_head && !(a.dbg & 4); ++li) {
+      const FusedHead& hd = a.H[li];
+      const float* hw = wsm + a.o_hw[li];
+      for (int e = tid; e < 32 * hd.n_pad; e += 256) {
+        const int ss = e / hd.n_pad, n = e - ss * hd.n_pad;
+        float v = 0.f;
+        if (n < hd.n_real) {
+          const float4* cr = reinterpret_cast<const float4*>(cur + ss * a.h_ld);
+          const float4* wr = reinterpret_cast<const float4*>(hw + n * hd.k_pad);
+          float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+          for (int kk = 0; kk < cur_w / 4; ++kk) {
+            const float4 c = cr[kk], w = wr[kk];
+            v0 = fmaf(c.x, w.x, v0);
+            v1 = fmaf(c.y, w.y, v1);
+            v2 = fmaf(c.z, w.z, v2);
+            v3 = fmaf(c.w, w.w, v3);
+          }
+          v = act_apply((v0 + v1) + (v2 + v3) + hd.bias[n], hd.act);
+        }
+        nxt[ss * a.h_ld + n] = v;
+      }
+      __syncthreads();
+      float* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+      cur_w = hd.n_pad;
+    }
+    if (tid < a.nr) a.out[(a.row0 + tid) * a.n_tgt + t] = cur[tid * a.h_ld + a.out_col];
+  }
+}
+
 // ------------------------------------------------------------------------------------ surrogate
 // train_model (wlm.py:132-278) in three stages:
 //  1. k_wlm_stats  (grid, block per Adam step): per-step constants that do not depend on w —
@@ -1914,21 +2476,6 @@ __device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lan
   return v[0] + __shfl_xor(v[0], 1);
 }
 
-// In-register 32 x 32 bit transpose: in a[i] bit b = M[i][b], out a[b] bit i = M[i][b].
-__device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
-#pragma unroll
-  for (int j = 16, s = 0; j != 0; j >>= 1, ++s) {
-    const uint32_t m = s == 0 ? 0x0000FFFFu : s == 1 ? 0x00FF00FFu : s == 2 ? 0x0F0F0F0Fu
-                     : s == 3 ? 0x33333333u : 0x55555555u;
-#pragma unroll
-    for (int k = 0; k < 32; k = (k + j + 1) & ~j) {
-      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
-      a[k + j] ^= t;
-      a[k] ^= t << j;
-    }
-  }
-}
-
 // x[i] = word `wd` of row row0 + i for i < nr, else 0.  row0 / nr are wave-uniform, so the row
 // test is a scalar branch and all loads are in flight together (no per-lane exec masking);
 // callers mask lanes past the chunk.
@@ -2355,6 +2902,221 @@ int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t r
   return 1;
 }
 
+int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 1;
+  }
+  return cus;
+}
+
+// Wide (full-graph) forward: 2-layer plans with large frontiers (returns 1 when it does not apply).
+struct WideWs {
+  size_t mT, mT0, kin, h1, total;
+  int nfi, a_ld, h_ld, o_h0, o_h1, o_e, kw;
+  int o_hw[kFusedMaxHead];
+  size_t lds;
+  bool gcn;
+};
+
+int wide_layout(const xpg_forward_plan* p, WideWs* W) {
+  if (p->n_layers != 2 || p->n_head > kFusedMaxHead || p->n_head < 0) return 1;
+  const xpg_layer_desc& l1 = p->layers[0];
+  const xpg_layer_desc& l2 = p->layers[1];
+  if (l1.n_terms < 1 || l1.n_terms > XPG_MAX_TERMS || l2.n_terms < 1 || l2.n_terms > XPG_MAX_TERMS) return 1;
+  for (int k = 0; k < l1.n_terms; ++k)
+    if (!l1.terms[k].table) return 1;
+  if (!l2.weight || l2.f_in_pad != l1.f_out_pad) return 1;
+  const int f1 = l1.f_out_pad;
+  W->nfi = f1 / 16;
+  if (f1 % 16) return 1;
+  if (W->nfi != 2 && W->nfi != 4 && W->nfi != 8 && W->nfi != 12 && W->nfi != 16) return 1;
+  const int K = l2.n_terms * l2.f_in_pad;
+  if (K % 16 || l2.f_out_pad % 32 || l2.f_out_pad > 256) return 1;
+  int hw = l2.f_out_pad, cur = l2.f_out_pad;
+  for (int i = 0; i < p->n_head; ++i) {
+    if (p->head[i].k_pad != cur || p->head[i].n_pad > 256) return 1;
+    hw = std::max(hw, p->head[i].n_pad);
+    cur = p->head[i].n_pad;
+  }
+  if (p->out_col < 0 || p->out_col >= cur) return 1;
+  W->gcn = false;  // kinT (kept in-degrees): GCN norms
+  for (int l = 0; l < 2; ++l)
+    for (int k = 0; k < p->layers[l].n_terms; ++k) W->gcn |= p->layers[l].terms[k].kind == XPG_TERM_GCN;
+  W->a_ld = K + 4;
+  W->h_ld = hw + 4;
+  W->o_h0 = 32 * W->a_ld;
+  int off_f = W->o_h0 + 32 * W->h_ld;
+  if (W->h_ld <= W->a_ld) {
+    W->o_h1 = 0;  // the second head tile reuses the A tile (dead after the MFMA)
+  } else {
+    W->o_h1 = off_f;
+    off_f += 32 * W->h_ld;
+  }
+  W->o_e = off_f;
+  off_f += 4 * kWideCap;
+  for (int i = 0; i < p->n_head; ++i) {
+    W->o_hw[i] = off_f;
+    off_f += (p->head[i].n_real * p->head[i].k_pad + 3) & ~3;
+  }
+  W->lds = sizeof(float) * (size_t)off_f;
+  if (W->lds > 150 * 1024) return 1;
+  W->kw = 0;  // layer weights in registers (one 32-column block per wave) when they fit
+  const char* kwe = getenv("XPG_WIDE_KW");
+  if (l2.f_out_pad <= 128 && (K == 32 || K == 64 || K == 128) && !(kwe && std::strcmp(kwe, "0") == 0))
+    W->kw = K / 8;
+  size_t off = 0;
+  W->mT = off;
+  off += align_up(sizeof(uint32_t) * (size_t)p->cols);
+  W->mT0 = off;
+  off += align_up(sizeof(uint32_t) * (size_t)p->n0);
+  W->kin = off;
+  off += align_up(W->gcn ? sizeof(float) * 32 * (size_t)p->n_rel * p->n0 : 0);
+  W->h1 = off;
+  off += align_up(sizeof(float) * 32 * (size_t)l1.n_tgt * f1);
+  W->total = off;
+  return 0;
+}
+
+bool wide_wanted(const xpg_forward_plan* p) {
+  const char* env = getenv("XPG_FORWARD");
+  if (env && std::strcmp(env, "wide") == 0) return true;
+  if (env && *env) return false;  // another path forced
+  return p->n_layers == 2 && p->layers[0].n_tgt >= 8192;
+}
+
+template <bool LAST>
+void (*wide_kernel(int nfi, int kw))(WideArgs) {
+#define XPG_WK(NFI, KW) \
+  if (nfi == NFI && kw == KW) return k_wide_tgt<NFI, LAST, KW>;
+  if constexpr (LAST) {
+    XPG_WK(2, 4) XPG_WK(2, 8) XPG_WK(4, 8) XPG_WK(4, 16) XPG_WK(8, 16)
+  }
+  XPG_WK(2, 0) XPG_WK(4, 0) XPG_WK(8, 0) XPG_WK(12, 0) XPG_WK(16, 0)
+#undef XPG_WK
+  return nullptr;
+}
+
+int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t* bits, int64_t rows, float* y,
+                     char* ws, hipStream_t st) {
+  const xpg_layer_desc& l1 = p->layers[0];
+  const xpg_layer_desc& l2 = p->layers[1];
+  const int words = words_of(p->cols);
+  uint32_t* mT = reinterpret_cast<uint32_t*>(ws + W.mT);
+  uint32_t* mT0 = reinterpret_cast<uint32_t*>(ws + W.mT0);
+  float* kinT = reinterpret_cast<float*>(ws + W.kin);
+  float* h1 = reinterpret_cast<float*>(ws + W.h1);
+  auto fill = [&](WideArgs& a, const xpg_layer_desc& ly) {
+    std::memset(&a, 0, sizeof(a));
+    a.n0 = p->n0;
+    a.n_rel = p->n_rel;
+    a.n_tgt = ly.n_tgt;
+    a.n_terms = ly.n_terms;
+    a.act = ly.act;
+    a.mT0 = mT0;
+    a.kinT = kinT;
+    a.tgt_prev = ly.tgt_prev;
+    a.tgt_f0 = ly.tgt_f0;
+    a.agg_ptr = ly.agg_ptr;
+    a.agg_src = ly.agg_src;
+    a.agg_f0 = ly.agg_f0;
+    a.self_mult = ly.self_mult;
+    a.bias = ly.bias;
+    int nagg = 0;
+    a.agg1 = -1;
+    for (int k = 0; k < ly.n_terms; ++k) {
+      a.kind[k] = ly.terms[k].kind;
+      a.rel[k] = ly.terms[k].rel;
+      a.table[k] = ly.terms[k].table;
+      if (a.kind[k] != XPG_TERM_ROOT) {
+        ++nagg;
+        a.agg1 = k;
+      }
+    }
+    if (nagg != 1) a.agg1 = -1;
+  };
+  WideArgs a1, a2;
+  fill(a1, l1);
+  const char* dbg = getenv("XPG_WIDE_DBG");
+  a1.dbg = dbg ? atoi(dbg) : 0;
+  a1.n_src = p->n0;
+  a1.w_row = l1.f_out_pad;
+  a1.f_real = l1.f_out;
+  a1.o_e = 0;
+  a1.out = h1;
+  fill(a2, l2);
+  a2.dbg = a1.dbg;
+  a2.n_src = l1.n_tgt;
+  a2.w_row = l2.f_in_pad;
+  a2.K = l2.n_terms * l2.f_in_pad;
+  a2.a_ld = W.a_ld;
+  a2.f_out = l2.f_out;
+  a2.f_out_pad = l2.f_out_pad;
+  a2.n_head = p->n_head;
+  a2.out_col = p->out_col;
+  a2.h_ld = W.h_ld;
+  a2.o_h0 = W.o_h0;
+  a2.o_h1 = W.o_h1;
+  a2.o_e = W.o_e;
+  for (int i = 0; i < p->n_head; ++i) {
+    a2.o_hw[i] = W.o_hw[i];
+    a2.H[i].k_pad = p->head[i].k_pad;
+    a2.H[i].n_real = p->head[i].n_real;
+    a2.H[i].n_pad = p->head[i].n_pad;
+    a2.H[i].act = p->head[i].act;
+    a2.H[i].weight = p->head[i].weight;
+    a2.H[i].bias = p->head[i].bias;
+  }
+  a2.weight = l2.weight;
+  a2.head1 = p->n_head == 1 && p->head[0].n_real == 1 && p->out_col == 0;
+  a2.src = h1;
+  a2.out = y;
+  void (*k1)(WideArgs) = wide_kernel<false>(l1.f_out_pad / 16, 0);
+  void (*k2)(WideArgs) = wide_kernel<true>(l2.f_in_pad / 16, W.kw);
+  if (!k1 || !k2) return fail(XPG_EINVAL, "wide forward: unsupported layer width");
+  const size_t lds1 = sizeof(float) * 3 * kWideCap;
+  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds1)));
+  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(W.lds)));
+  const int cus = device_cus();
+  // persistent grids sized to residency (static target striding: no late starters)
+  int per_cu1 = 0, per_cu2 = 0;
+  XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, reinterpret_cast<const void*>(k1), 256, lds1));
+  XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, reinterpret_cast<const void*>(k2), 256, W.lds));
+  per_cu1 = std::max(1, per_cu1);
+  per_cu2 = std::max(1, per_cu2);
+  const unsigned g1 = static_cast<unsigned>(std::min<int64_t>(l1.n_tgt, per_cu1 * (int64_t)cus));
+  const unsigned g2 = static_cast<unsigned>(std::min<int64_t>(l2.n_tgt, per_cu2 * (int64_t)cus));
+  for (int64_t r0 = 0; r0 < rows; r0 += kWideS) {
+    const int nr = static_cast<int>(std::min<int64_t>(kWideS, rows - r0));
+    hipLaunchKernelGGL(k_wide_bits, dim3(static_cast<unsigned>(cdiv(words, 256))), dim3(256), 0, st, bits, r0, nr,
+                       words, p->cols, mT);
+    XPG_LAUNCHED();
+    hipLaunchKernelGGL(k_wide_f0, dim3(static_cast<unsigned>(cdiv(p->n0, 256))), dim3(256), 0, st, mT, p->f0_node,
+                       p->n0, mT0);
+    XPG_LAUNCHED();
+    if (W.gcn) {
+      const int64_t n = (int64_t)p->n_rel * p->n0 * 32;
+      hipLaunchKernelGGL(k_wide_degree, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, st, mT, mT0, p->n0,
+                         p->n_rel, p->deg_ptr, p->deg_src, kinT);
+      XPG_LAUNCHED();
+    }
+    a1.nr = nr;
+    a1.row0 = r0;
+    hipLaunchKernelGGL(k1, dim3(g1), dim3(256), lds1, st, a1);
+    XPG_LAUNCHED();
+    a2.nr = nr;
+    a2.row0 = r0;
+    hipLaunchKernelGGL(k2, dim3(g2), dim3(256), W.lds, st, a2);
+    XPG_LAUNCHED();
+  }
+  return XPG_OK;
+}
+
 // Lanes-=-rows fused forward for 1- and 2-layer plans (returns 1 when it does not apply).
 int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
   if (p->n_layers < 1 || p->n_layers > 2 || p->n_head > kFusedMaxHead) return 1;
@@ -2601,6 +3363,11 @@ int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* by
   WsLayout L;
   int rc = layout_ws(plan, rows, &L);
   if (rc) return rc;
+  WideWs W;
+  if (wide_wanted(plan) && wide_layout(plan, &W) == 0) {
+    *bytes = W.total;  // independent of rows: 32-row passes
+    return XPG_OK;
+  }
   *bytes = L.total;
   return XPG_OK;
 }
@@ -2610,10 +3377,18 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   WsLayout L;
   int rc = layout_ws(p, rows, &L);
   if (rc) return rc;
-  XPG_REQ(workspace_bytes >= L.total, "masked_forward: workspace too small");
   XPG_REQ(p->n_rel >= 1 && p->n0 >= 1 && p->cols > 0, "masked_forward: bad plan sizes");
-  if (rows == 0) return XPG_OK;
   hipStream_t st = S(stream);
+  {
+    WideWs W;
+    if (wide_wanted(p) && wide_layout(p, &W) == 0) {
+      XPG_REQ(workspace_bytes >= W.total, "masked_forward: workspace too small");
+      if (rows == 0) return XPG_OK;
+      return run_wide_forward(p, W, bits, rows, y, static_cast<char*>(workspace), st);
+    }
+  }
+  XPG_REQ(workspace_bytes >= L.total, "masked_forward: workspace too small");
+  if (rows == 0) return XPG_OK;
   {
     const char* env = getenv("XPG_FORWARD");
     const bool multi = env && std::strcmp(env, "unfused") == 0;
@@ -2725,16 +3500,6 @@ static bool wlm_env(const char* v) {
 }
 static bool wlm_force_grid() { return wlm_env("grid"); }
 
-static int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 1;
-  }
-  return cus;
-}
 
 // Word slices per wave item: minimise (rounds of 16 waves) x (words per item + 1 for the item's
 // fixed cost) over blocks x slices items.

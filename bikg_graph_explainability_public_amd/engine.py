@@ -303,8 +303,11 @@ class ForwardPlan:
         y = torch.empty((rows, self.n_out), dtype=torch.float32, device=self.device)
         if rows == 0:
             return y
-        per_row = max(1, self.workspace_bytes(1))
-        chunk = max(1, min(rows, max_ws_bytes // per_row))
+        w1, w2 = self.workspace_bytes(1), self.workspace_bytes(2)
+        per_row = max(0, w2 - w1)  # 0: a rows-independent workspace (the wide 32-row passes)
+        fixed = max(0, w1 - per_row)
+        chunk = rows if per_row == 0 else \
+            max(1, min(rows, max(0, max_ws_bytes - fixed) // per_row))
         need = self.workspace_bytes(chunk)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)

@@ -29,11 +29,13 @@ def _eng():
     return engine
 
 
-@pytest.fixture(params=["rows", "fused", "unfused"])
+@pytest.fixture(params=["rows", "fused", "unfused", "wide"])
 def fwd_path(request, monkeypatch):
-    """xpg_masked_forward has three HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
-    (default), the wave-per-row fused kernel (XPG_FORWARD=fused) and the multi-kernel path
-    (XPG_FORWARD=unfused, also the fallback for plans the fused kernels do not take)."""
+    """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
+    (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
+    32-samples-per-pass wide path for 2-layer plans (XPG_FORWARD=wide; default for frontiers of
+    8192+ nodes) and the multi-kernel path (XPG_FORWARD=unfused, also the fallback for plans the
+    others do not take)."""
     monkeypatch.setenv("XPG_FORWARD", request.param)
     return request.param
 
@@ -201,6 +203,41 @@ def test_masked_forward_synthetic_archs(kind, dims, fc, fwd_path):
     ref = oracle.masked_query_outputs(spec, x.numpy(), {None: ei.numpy()}, m, q)
     got = plan.forward(e.pack_masks(torch.as_tensor(m).to(DEV)))[:, 0].cpu().numpy()
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind,dims,fc", [("gcn", [16, 32, 32], [32, 1]),
+                                           ("sage", [16, 64, 64], [64, 8, 1]),
+                                           ("sage", [24, 128, 128], [128, 1]),
+                                           ("gcn", [16, 64, 128], [128, 16, 1])])
+def test_full_graph_forward_all_targets(kind, dims, fc, fwd_path):
+    """Every node a target (the full-graph regime): outputs of all S nodes per
+    mask row in one plan, vs the fp64 oracle run per query, on a graph with self-loops and
+    duplicate edges; 70 rows = two full 32-sample passes of the wide path plus a partial one."""
+    from golden_utils import oracle_spec
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    e = _eng()
+    g = torch.Generator().manual_seed(23)
+    S, E = 400, 2400
+    x = torch.randn((S, dims[0]), generator=g)
+    ei = torch.randint(0, S, (2, E), generator=g)
+    ei[:, :25] = ei[0, :25]  # self-loops
+    ei[:, 25:50] = ei[:, 50:75]  # duplicate edges
+    torch.manual_seed(4)
+    arch = ConvStack(kind, dims, fc).eval()
+    plan = pipeline.build_plan(arch.to(DEV), x.to(DEV), ei.to(DEV), list(range(S)))
+    spec = oracle_spec({"arch_spec": {"kind": kind, "dims": dims, "fc": fc}},
+                       {k: v.detach().cpu().numpy() for k, v in arch.state_dict().items()})
+    rng = np.random.default_rng(9)
+    m = rng.random((70, S)) < rng.random((70, 1))
+    m[0] = True
+    m[1] = False
+    got = plan.forward(e.pack_masks(torch.as_tensor(m).to(DEV))).cpu().numpy()
+    assert got.shape == (70, S)
+    pos = plan.frontiers[-1]  # output column i is node pos[i]
+    for i in list(range(0, S, 37)) + [S - 1]:
+        ref = oracle.masked_query_outputs(spec, x.numpy(), {None: ei.numpy()}, m, int(pos[i]))
+        np.testing.assert_allclose(got[:, i], ref, rtol=0, atol=1e-5)
 
 
 def test_generic_path_matches_engine():

@@ -91,8 +91,12 @@ def main():
         print(f"[B] plan (all targets): n0={plan.n0} in {time.time() - t0:.1f}s", flush=True)
         rb = args.rows_b
         bits = engine.sample_shapley(13, rb, N, dev)
-        ms, y = timed(lambda: plan.forward(bits), reps=2)
-        print(f"[B] full forward {rb} rows x {N} targets: {ms:.3f} ms = {ms / rb:.3f} ms/row", flush=True)
+        for dbg in ("0", "1", "2", "3", "4", "8", "12"):
+            os.environ["XPG_WIDE_DBG"] = dbg
+            ms, y = timed(lambda: plan.forward(bits), reps=2)
+            print(f"[B] full forward (XPG_WIDE_DBG={dbg}) {rb} rows x {N} targets: {ms:.3f} ms = "
+                  f"{ms / rb:.3f} ms/row", flush=True)
+        os.environ["XPG_WIDE_DBG"] = "0"
 
 
 if __name__ == "__main__":
