@@ -46,6 +46,10 @@ def parse():
                    help="Explainer.run(times=...) repeats per rank per step (batched fits)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=12800)
+    p.add_argument("--full-graph-rows", type=int, default=64,
+                   help="regime (ii): mask rows of the c3-shaped full-graph forward (0 = skip)")
+    p.add_argument("--no-graph-prediction", action="store_true",
+                   help="skip the c3 graph_prediction per-query pipeline section")
     return p.parse_args()
 
 
@@ -154,6 +158,166 @@ def cpu_baseline(args, arch, sub_feat, sub_ei, q):
     return {"value": rows / dt, "unit": "samples/s", "cores": 1, "kind": "port",
             "sample": f"{rows} mask rows of the same workload (S={S}) through the numpy oracle "
                       f"(union-graph forward + KernelSHAP + surrogate fit), {dt:.1f} s"}
+
+
+def c3_graph(dev, nodes=1_000_000, edges=10_000_000, feat=128, seed=0):
+    """synthetic homogeneous graph, 2-layer SAGEConv(mean) 128-128-128, head
+    Linear(128, 1) + sigmoid (random init, ConvStack layout of the reference tests)."""
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((nodes, feat), generator=g)
+    ei = torch.randint(0, nodes, (2, edges), generator=g)
+    torch.manual_seed(seed)
+    arch = ConvStack("sage", [feat, feat, feat], [feat, 1]).eval()
+    return x, ei, arch
+
+
+def full_graph_bytes(n, e_kept_per_row, e, f_in, f_out, rows, layers=2):
+    """SURVEY.md §8d algorithmic bytes per sample of the full-graph masked forward, summed over
+    the rows: per layer 4(N+1) + 4E (CSR) + N/8 (mask bits) + 4 F_g E_kept (gathered rows,
+    F_g = min(F_in, F_out)) + 4 F_root N (SAGE self rows) + 4 F_out N (layer output)."""
+    per_layer_fixed = 4 * (n + 1) + 4 * e + n / 8 + 4 * f_in * n + 4 * f_out * n
+    return layers * (per_layer_fixed * rows + 4 * min(f_in, f_out) * e_kept_per_row.sum())
+
+
+def full_graph_section(args, dev):
+    """Regime (ii): every node a target of the masked forward on the c3 graph
+    (1M nodes / 10M edges / 128 features / 2-layer SAGE), `rows` mask rows (32-sample passes)."""
+    from bikg_graph_explainability_public_amd import engine, pipeline
+    x, ei, arch = c3_graph(dev)
+    N, E = x.shape[0], ei.shape[1]
+    xd, eid = x.to(dev), ei.to(dev)
+    arch = arch.to(dev)
+    plan = pipeline.build_plan(arch, xd, eid, list(range(N)))
+    rows = args.full_graph_rows
+    bits = engine.sample_shapley(77, rows, N, dev)
+    y = plan.forward(bits)  # warm-up (workspace, code objects)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 3
+    a.record(stream)
+    for _ in range(reps):
+        y = plan.forward(bits)
+    b.record(stream)
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    # kept edges per row (both endpoints active), for the algorithmic byte count
+    m = engine.unpack_masks(bits, N)
+    kept = (m[:, eid[0]] & m[:, eid[1]]).sum(1).double().cpu().numpy()
+    del m
+    bytes_ = full_graph_bytes(N, kept, E, 128, 128, rows)
+    flops = rows * N * 2.0 * (2 * 128 * 128 + 128)  # layer-2 dense (l and r) + head, per target
+    achieved = bytes_ / (ms * 1e-3) / 1e9
+    out = {
+        "workload": "c3 full-graph masked forward (SURVEY.md §8d regime (ii)): 1M nodes / 10M "
+                    "edges, 128 feats, 2-layer SAGEConv(mean) + Linear(128,1) + sigmoid, every "
+                    "node a target (all 1M outputs per mask row)",
+        "rows": rows, "ms": ms, "ms_per_row": ms / rows,
+        "samples_per_s": rows / (ms * 1e-3),
+        "node_outputs_per_s": rows * N / (ms * 1e-3),
+        "roofline": {"kernel": "wide forward chain (k_wide_bits, k_wide_f0, k_wide_tgt<layer 1>, "
+                               "k_wide_tgt<layer 2 + head>)",
+                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": bytes_,
+                     "bytes_formula": "SURVEY.md §8d B_alg per sample, E_kept measured per row"},
+        "mfma": {"tflops": flops / (ms * 1e-3) / 1e12, "peak_fp32_tflops": 157.3,
+                 "frac": flops / (ms * 1e-3) / 1e12 / 157.3},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = full_graph_cpu(arch)
+    return out
+
+
+def full_graph_cpu(arch):
+    """The numpy oracle (1 thread) on ONE mask row of the same model on a 1/10-scale c3 graph
+    (100k nodes / 1M edges, same degree and widths): the forward is linear in N and E, so the
+    per-sample rate at full scale is the measured one / 10 (reported as such)."""
+    import oracle
+    try:
+        from threadpoolctl import threadpool_limits
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+    x, ei, _ = c3_graph("cpu", nodes=100_000, edges=1_000_000)
+    sd = {k: v.detach().cpu().numpy() for k, v in arch.state_dict().items()}
+    spec = {"convs": [{"kind": "sage", "rels": [None], "act": "relu",
+                       "params": {None: {"Wl": sd[f"conv.{2 * i}.lin_l.weight"],
+                                         "bl": sd[f"conv.{2 * i}.lin_l.bias"],
+                                         "Wr": sd[f"conv.{2 * i}.lin_r.weight"]}}}
+                      for i in range(2)],
+            "fc": [{"W": sd["fc.0.weight"], "b": sd["fc.0.bias"], "act": "sigmoid"}]}
+    rng = np.random.default_rng(0)
+    m = rng.random(x.shape[0]) < 0.5
+    e = ei.numpy()
+    keep = m[e[0]] & m[e[1]]
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    try:
+        t0 = time.perf_counter()
+        oracle.forward_union(spec, x.numpy(), {None: (e[0][keep], e[1][keep])}, dtype=np.float32)
+        dt = time.perf_counter() - t0
+    finally:
+        if ctx is not None and hasattr(ctx, "unregister"):
+            ctx.unregister()
+    return {"value": 1.0 / (dt * 10), "unit": "samples/s", "cores": 1, "kind": "port",
+            "sample": f"1 mask row through the numpy oracle on a 1/10-scale c3 graph (100k nodes / "
+                      f"1M edges) in {dt:.1f} s; full-scale rate = 1 / (10 x {dt:.1f} s)"}
+
+
+def graph_prediction_section(args, dev):
+    """The reference's graph_prediction semantics on the c3 graph (explainer.py:427-447: no
+    subgraph, S = N = 1M mask columns) for one query node, one repeat of interpret_samples=512,
+    epochs=50 (25,600 rows): device sampler with fused row counts -> receptive-field forward ->
+    KernelSHAP -> many-column surrogate fit (k_gw_*: streams the step's mask bits twice)."""
+    from bikg_graph_explainability_public_amd import engine, pipeline
+    x, ei, arch = c3_graph(dev)
+    N = x.shape[0]
+    plan = pipeline.build_plan(arch.to(dev), x.to(dev), ei.to(dev), [7])
+    R, epochs = 512 * 50, 50
+    batch = R // epochs
+    w0 = torch.zeros(N, device=dev)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    stream = torch.cuda.current_stream()
+
+    def rep(i, ev=None):
+        if ev:
+            ev[0].record(stream)
+        bits, cnt = engine.sample_shapley(500 + i, R, N, dev, with_counts=True)
+        if ev:
+            ev[1].record(stream)
+        y = plan.forward(bits)[:, 0]
+        if ev:
+            ev[2].record(stream)
+        k = engine.shap_kernel(bits, N, counts=cnt)
+        if ev:
+            ev[3].record(stream)
+        engine.wlm_fit(bits, N, batch, y, k, w0, params)
+        if ev:
+            ev[4].record(stream)
+
+    rep(0)
+    torch.cuda.synchronize()
+    reps = 3
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(reps)]
+    for i in range(reps):
+        rep(1 + i, evs[i])
+    torch.cuda.synchronize()
+    ph = {name: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in evs]))
+          for j, name in enumerate(("sample", "forward", "shap", "wlm"))}
+    total = sum(ph.values())
+    W = (N + 31) // 32
+    wbytes = 2 * R * W * 4 + epochs * 6 * N * 4  # mask bits twice per step + Adam state r/w
+    return {"workload": "c3 graph_prediction, one query (node 7), S = 1M mask columns, "
+                        "interpret_samples=512 x epochs=50 = 25,600 rows, one repeat",
+            "ms_per_repeat": total, "samples_per_s": R / (total * 1e-3), "phases_ms": ph,
+            "roofline": {"kernel": "many-column surrogate fit (k_wlm_stats, k_gw_p, k_gw_g, "
+                                   "k_gw_grad, k_gw_loss)", "bound": "hbm",
+                         "achieved": wbytes / (ph["wlm"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s",
+                         "frac": wbytes / (ph["wlm"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "bytes_per_launch": wbytes,
+                         "bytes_formula": "2 x R x ceil(S/32) x 4 (bits, p and grad passes) + "
+                                          "steps x 24 S (w, m, v read + write)"},
+            "sampler_GBps": R * W * 4 / (ph["sample"] * 1e-3) / 1e9}
 
 
 def main():
@@ -270,6 +434,18 @@ def main():
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, arch, sub_feat, sub_ei, q)
+        if world == 1:
+            del plan
+            torch.cuda.empty_cache()
+            regimes = {}
+            if not args.no_graph_prediction:
+                regimes["graph_prediction_c3"] = graph_prediction_section(args, dev)
+                torch.cuda.empty_cache()
+            if args.full_graph_rows > 0:
+                regimes["full_graph_c3"] = full_graph_section(args, dev)
+                torch.cuda.empty_cache()
+            if regimes:
+                line["regimes"] = regimes
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
