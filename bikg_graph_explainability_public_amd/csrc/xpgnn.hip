@@ -1227,13 +1227,14 @@ struct WideArgs {
   int64_t row0;  // global index of the block's first mask row (output rows of the last layer)
   int nr, n0, n_src, n_tgt, n_rel, n_terms, w_row, f_real, act;
   int agg1;  // the only aggregating (non-ROOT) term, or -1 when there are several
+  int64_t rstride;  // floats between consecutive source rows: w_row (tables) or 32 w_row (h1)
   int head1;  // the head is one Linear(f_out, 1) (+ act) read at column 0: fused epilogue
   int dbg;   // diagnostics (XPG_WIDE_DBG): 1 skip dense + head, 2 skip row gathers, 4 head, 8 dense
   int K, a_ld, f_out, f_out_pad, n_head, out_col, h_ld, o_h0, o_h1, o_e;
   int o_hw[kFusedMaxHead];
   const uint32_t* mT0;
   const float* kinT;
-  const float* src;  // last layer: h1 [32][n_src][w_row]
+  const float* src;  // last layer: h1 [n_src][32][w_row]
   const float* table[XPG_MAX_TERMS];  // layer 1: X W_k^T [n0][w_row]
   const int32_t* tgt_prev;
   const int32_t* tgt_f0;
@@ -1245,7 +1246,7 @@ struct WideArgs {
   const float* bias;
   int kind[XPG_MAX_TERMS], rel[XPG_MAX_TERMS];
   FusedHead H[kFusedMaxHead];
-  float* out;  // layer 1: h1 [32][n_tgt][w_row]; last layer: y [rows][n_tgt]
+  float* out;  // layer 1: h1 [n_tgt][32][w_row] (node-major); last layer: y [rows][n_tgt]
 };
 
 constexpr int kWideCap = 256;  // staged in-edges per target (all terms, one per thread); more: in place
@@ -1284,7 +1285,7 @@ __device__ __forceinline__ int wide_gather_rows(const WideArgs& a, int k, int e0
 #pragma unroll
       for (int i = 0; i < NFI; ++i) rr[j][i] = 0.f;
       if (cf[j] != 0.f) {
-        const float* sp = base + (int64_t)row[j] * a.w_row + fo;
+        const float* sp = base + (int64_t)row[j] * a.rstride + fo;
         if (NFI % 4 == 0) {
 #pragma unroll
           for (int i = 0; i < NFI / 4; ++i) {
@@ -1351,7 +1352,7 @@ __device__ __forceinline__ void wide_gather2(const WideArgs& a, int e0, int e1, 
         if (j >= 0) {
           const int ee = c0 + j;
           const float* bp = first ? base0 : base1;
-          const float* sp = bp + (int64_t)Esrc[ee] * a.w_row + fo;
+          const float* sp = bp + (int64_t)Esrc[ee] * a.rstride + fo;
           const int sidx = first ? s0 : s1;
           const float c = kind == XPG_TERM_GCN
                               ? (first ? dt0 : dt1) * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + Eu0[ee]) * 32 + sidx])
@@ -1384,6 +1385,177 @@ __device__ __forceinline__ void wide_gather2(const WideArgs& a, int e0, int e1, 
           acc0[i] = fmaf(c0v[q], rr[q][i], acc0[i]);
           acc1[i] = fmaf(c1v[q], rr[q][i], acc1[i]);
         }
+    }
+  }
+}
+
+// Layer 1 of the wide path on the matrix cores.  Features are never masked (data.py:582), so
+// for a target t every term's aggregate over the 32 samples is a 0/1-weighted sum of SHARED
+// table rows: h1[s][t] = act(b + sum_entries coef[s][e] T_k(e)[row(e)]), entries = the kept-able
+// in-edges of each term plus one self entry per term (GCN dt^2, SAGE self-loop multiplicity,
+// ROOT), coef = keep_s x (MEAN: 1 / max(cnt_s + sm, 1); GCN: dt_s dinv_u,s).  That is a
+// [32 samples x entries] x [entries x f_pad] product: v_mfma_f32_32x32x2_f32 with the per-sample
+// coefficients as the A operand and each table row read ONCE per 32 samples as the B operand.
+// Workgroup = one target (persistent), wave = 32-column blocks.  Exact fp32 products, fixed
+// accumulation order.
+constexpr int kL1Cap = 128;  // entries per target staged in LDS per round (more: chunked)
+
+// 512 threads: waves 0-3 stage, build coefficients and run the MFMAs into an LDS tile; waves 4-7
+// copy the finished tile to h1 with coalesced stores.  The roles are split because vmcnt counts
+// loads and stores in order: a wave that stored target t would wait for those stores before
+// using its loads of target t + 1.  Barriers are plain s_barrier (LDS drained by lgkmcnt), never
+// a fence on global memory, so the store waves never wait for their stores either.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+__global__ __launch_bounds__(512) void k_wide_l1m(const WideArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float ctile[];  // [32][w_row + 4]
+  __shared__ const float* Eptr[kL1Cap];       // table row of the entry
+  __shared__ float coefA[kL1Cap][33];         // per-sample coefficient (the MFMA A operand)
+  __shared__ int Eu0[kL1Cap], Ek[kL1Cap];
+  __shared__ uint32_t Em[kL1Cap];             // keep word (edge) or 0xFFFFFFFF (self entry)
+  __shared__ float invc[XPG_MAX_TERMS][32];   // MEAN: 1 / max(cnt_s + sm, 1), 0 if t masked in s
+  __shared__ float dts[XPG_MAX_TERMS][32];    // GCN: dt_s
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i32 = lane & 31, h = lane >> 5;
+  const int cld = a.w_row + 4;
+  const bool storer = wave >= 4;
+  __shared__ int nch_s;  // entry chunks of the current target (the store waves' barrier count)
+  int prev_t = -1;
+  const int mine = blockIdx.x < a.n_tgt ? (a.n_tgt - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  for (int it = 0; it <= mine; ++it) {  // one extra round drains the last tile
+    const int t = blockIdx.x + it * gridDim.x;
+    const bool have = it < mine;
+    if (storer) {  // ---- copy the previous target's tile to h1 (rows < nr); no global loads here
+      if (prev_t >= 0) {
+        const int q4 = a.w_row / 4;
+        for (int e = tid - 256; e < a.nr * q4; e += 256) {
+          const int row = e / q4, c4 = e - row * q4;
+          const float4 v = *reinterpret_cast<const float4*>(ctile + row * cld + 4 * c4);
+          *reinterpret_cast<float4*>(a.out + ((int64_t)prev_t * 32 + row) * a.w_row + 4 * c4) = v;
+        }
+      }
+      lds_barrier();  // tile read; nch_s published
+      const int rounds = 3 * nch_s;
+      for (int i = 0; i < rounds; ++i) lds_barrier();
+      prev_t = t;
+      continue;
+    }
+    const int tf0 = have ? a.tgt_f0[t] : 0;
+    const uint32_t mv = have ? a.mT0[tf0] : 0u;
+    int total = 0;  // entries: every non-root term's in-edges, + 1 self entry per term
+    if (have)
+      for (int k = 0; k < a.n_terms; ++k) {
+        if (a.kind[k] != XPG_TERM_ROOT) {
+          const int32_t* pp = a.agg_ptr + (int64_t)a.rel[k] * (a.n_tgt + 1);
+          total += pp[t + 1] - pp[t];
+        }
+        total += 1;
+      }
+    if (tid == 0) nch_s = (total + kL1Cap - 1) / kL1Cap;
+    lds_barrier();  // the store waves have read the previous tile
+    if (!have) continue;
+    if (tid < 32 * a.n_terms) {  // per-term, per-sample normalisers (thread = (term, sample))
+      const int k = tid >> 5, sidx = tid & 31;
+      const bool tk = (mv >> sidx) & 1u;
+      if (a.kind[k] == XPG_TERM_MEAN) {  // kept in-degree from the degree pass
+        const int cnt = static_cast<int>(a.kinT[((int64_t)a.rel[k] * a.n0 + tf0) * 32 + sidx]);
+        const int sm = a.self_mult[(int64_t)a.rel[k] * a.n_tgt + t];
+        invc[k][sidx] = tk ? 1.f / static_cast<float>(max(cnt + sm, 1)) : 0.f;
+      } else if (a.kind[k] == XPG_TERM_GCN) {
+        dts[k][sidx] = inv_sqrt_deg(a.kinT[((int64_t)a.rel[k] * a.n0 + tf0) * 32 + sidx]);
+      }
+    }
+    for (int c0 = 0; c0 < total; c0 += kL1Cap) {
+      const int nent = min(kL1Cap, total - c0);
+      // ---- stage entries [c0, c0 + nent) in term order (a term's edges, then its self entry)
+      if (tid < kL1Cap) {
+        const int i = tid;
+        if (i < nent) {
+          int gi = c0 + i, k = 0;
+          for (;; ++k) {
+            const int len = (a.kind[k] == XPG_TERM_ROOT ? 0 : a.agg_ptr[(int64_t)a.rel[k] * (a.n_tgt + 1) + t + 1] -
+                                                                a.agg_ptr[(int64_t)a.rel[k] * (a.n_tgt + 1) + t]) + 1;
+            if (gi < len) break;
+            gi -= len;
+          }
+          const int len_e = a.kind[k] == XPG_TERM_ROOT ? 0 : a.agg_ptr[(int64_t)a.rel[k] * (a.n_tgt + 1) + t + 1] -
+                                                                a.agg_ptr[(int64_t)a.rel[k] * (a.n_tgt + 1) + t];
+          int u0 = tf0;
+          uint32_t m = 0xFFFFFFFFu;
+          if (gi < len_e) {
+            u0 = a.agg_f0[a.agg_ptr[(int64_t)a.rel[k] * (a.n_tgt + 1) + t] + gi];
+            m = a.mT0[u0] & mv;  // kept iff both endpoints active
+          }
+          Ek[i] = k;
+          Eu0[i] = u0;
+          Em[i] = m;
+          Eptr[i] = a.table[k] + (int64_t)u0 * a.w_row;
+        } else {
+          Ek[i] = 0;
+          Eu0[i] = tf0;
+          Em[i] = 0u;
+          Eptr[i] = a.table[0];  // a valid row, coefficient 0
+        }
+      }
+      lds_barrier();
+      // ---- coefficients: thread = (entry, sample), branch-free for the MFMA rounds below
+      for (int q = tid; q < kL1Cap * 32; q += 256) {
+        const int e = q >> 5, sidx = q & 31;
+        float c = 0.f;
+        if (e < nent) {
+          const int k = Ek[e], kind = a.kind[k];
+          const uint32_t m = Em[e];
+          const bool self = m == 0xFFFFFFFFu;
+          if (kind == XPG_TERM_ROOT) {
+            c = 1.f;
+          } else if (kind == XPG_TERM_MEAN) {
+            c = self ? static_cast<float>(a.self_mult[(int64_t)a.rel[k] * a.n_tgt + t]) * invc[k][sidx]
+                     : (((m >> sidx) & 1u) ? invc[k][sidx] : 0.f);
+          } else {  // GCN
+            const float dt = dts[k][sidx];
+            c = self ? dt * dt
+                     : (((m >> sidx) & 1u) ? dt * inv_sqrt_deg(a.kinT[((int64_t)a.rel[k] * a.n0 + Eu0[e]) * 32 + sidx])
+                                           : 0.f);
+          }
+        }
+        coefA[e][sidx] = c;
+      }
+      lds_barrier();
+      const int nr16 = (nent + 15) & ~15;
+      for (int nb = wave; nb * 32 < a.w_row; nb += 4) {
+        const int col = nb * 32 + i32;
+        f32x16 acc;
+        if (c0 == 0) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        } else {  // continue a chunked target (high in-degree, rare): partial sums from the tile
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q] = ctile[((q & 3) + 8 * (q >> 2) + 4 * h) * cld + col];
+        }
+        for (int e0 = 0; e0 < nr16; e0 += 16) {  // 8 MFMAs (16 entries) per round, loads first
+          float av[8], bv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int e = e0 + 2 * j + h;
+            bv[j] = Eptr[e][col];
+            av[j] = coefA[e][i32];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], bv[j], acc, 0, 0, 0);
+        }
+        const bool last_chunk = c0 + nent >= total;
+        const float bias = (last_chunk && col < a.f_real) ? a.bias[col] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          float v = acc[q];
+          if (last_chunk) v = col < a.f_real ? act_apply(v + bias, a.act) : 0.f;
+          ctile[((q & 3) + 8 * (q >> 2) + 4 * h) * cld + col] = v;
+        }
+      }
+      lds_barrier();
     }
   }
 }
@@ -1497,12 +1669,12 @@ __global__ __launch_bounds__(256, LAST ? 2 : (NFI >= 12 ? 2 : 3)) void k_wide_tg
       for (int i = 0; i < NFI; ++i) tot0[i] = tot1[i] = 0.f;
       for (int k = 0; k < a.n_terms; ++k) {
         const int kind = a.kind[k], r = a.rel[k];
-        const float* base0 = LAST ? a.src + (int64_t)(v0 ? s0 : 0) * a.n_src * a.w_row : a.table[k];
-        const float* base1 = LAST ? a.src + (int64_t)(v1 ? s1 : 0) * a.n_src * a.w_row : a.table[k];
+        const float* base0 = LAST ? a.src + (int64_t)(v0 ? s0 : 0) * a.w_row : a.table[k];
+        const float* base1 = LAST ? a.src + (int64_t)(v1 ? s1 : 0) * a.w_row : a.table[k];
         float self0[NFI], self1[NFI];
         {
-          const float* p0r = base0 + (int64_t)tp * a.w_row + fo;
-          const float* p1r = base1 + (int64_t)tp * a.w_row + fo;
+          const float* p0r = base0 + (int64_t)tp * a.rstride + fo;
+          const float* p1r = base1 + (int64_t)tp * a.rstride + fo;
 #pragma unroll
           for (int i = 0; i < NFI; ++i) {
             self0[i] = p0r[i];
@@ -1579,12 +1751,12 @@ __global__ __launch_bounds__(256, LAST ? 2 : (NFI >= 12 ? 2 : 3)) void k_wide_tg
           o1[i] = f < a.f_real ? act_apply(tot1[i] + bv, a.act) : 0.f;
         }
         if (v0) {
-          float* o = a.out + ((int64_t)s0 * a.n_tgt + t) * a.w_row + fo;
+          float* o = a.out + ((int64_t)t * 32 + s0) * a.w_row + fo;
 #pragma unroll
           for (int i = 0; i < NFI; ++i) o[i] = o0[i];
         }
         if (v1) {
-          float* o = a.out + ((int64_t)s1 * a.n_tgt + t) * a.w_row + fo;
+          float* o = a.out + ((int64_t)t * 32 + s1) * a.w_row + fo;
 #pragma unroll
           for (int i = 0; i < NFI; ++i) o[i] = o1[i];
         }
@@ -2943,9 +3115,10 @@ int wide_layout(const xpg_forward_plan* p, WideWs* W) {
     cur = p->head[i].n_pad;
   }
   if (p->out_col < 0 || p->out_col >= cur) return 1;
-  W->gcn = false;  // kinT (kept in-degrees): GCN norms
+  W->gcn = false;  // kinT (kept in-degrees): GCN norms, layer-1 MEAN counts
   for (int l = 0; l < 2; ++l)
-    for (int k = 0; k < p->layers[l].n_terms; ++k) W->gcn |= p->layers[l].terms[k].kind == XPG_TERM_GCN;
+    for (int k = 0; k < p->layers[l].n_terms; ++k)
+      W->gcn |= p->layers[l].terms[k].kind == XPG_TERM_GCN || (l == 0 && p->layers[l].terms[k].kind == XPG_TERM_MEAN);
   W->a_ld = K + 4;
   W->h_ld = hw + 4;
   W->o_h0 = 32 * W->a_ld;
@@ -3044,6 +3217,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   a1.dbg = dbg ? atoi(dbg) : 0;
   a1.n_src = p->n0;
   a1.w_row = l1.f_out_pad;
+  a1.rstride = l1.f_out_pad;
   a1.f_real = l1.f_out;
   a1.o_e = 0;
   a1.out = h1;
@@ -3051,6 +3225,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   a2.dbg = a1.dbg;
   a2.n_src = l1.n_tgt;
   a2.w_row = l2.f_in_pad;
+  a2.rstride = 32 * (int64_t)l2.f_in_pad;  // h1 is node-major: [n1][32 samples][w_row]
   a2.K = l2.n_terms * l2.f_in_pad;
   a2.a_ld = W.a_ld;
   a2.f_out = l2.f_out;
@@ -3074,10 +3249,16 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   a2.head1 = p->n_head == 1 && p->head[0].n_real == 1 && p->out_col == 0;
   a2.src = h1;
   a2.out = y;
-  void (*k1)(WideArgs) = wide_kernel<false>(l1.f_out_pad / 16, 0);
+  // layer 1: the lane-group gather kernel (default, faster on MI355X at c3) or the MFMA formulation
+  // (XPG_WIDE_L1=mfma; kept as the second implementation both parity suites run)
+  const char* l1e = getenv("XPG_WIDE_L1");
+  void (*k1)(WideArgs) = (l1e && std::strcmp(l1e, "mfma") == 0) ? k_wide_l1m
+                                                                 : wide_kernel<false>(l1.f_out_pad / 16, 0);
   void (*k2)(WideArgs) = wide_kernel<true>(l2.f_in_pad / 16, W.kw);
   if (!k1 || !k2) return fail(XPG_EINVAL, "wide forward: unsupported layer width");
-  const size_t lds1 = sizeof(float) * 3 * kWideCap;
+  const bool l1m = k1 == k_wide_l1m;
+  const size_t lds1 = l1m ? sizeof(float) * 32 * (size_t)(l1.f_out_pad + 4) : sizeof(float) * 3 * kWideCap;
+  const int thr1 = l1m ? 512 : 256;
   XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds1)));
   XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3085,7 +3266,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const int cus = device_cus();
   // persistent grids sized to residency (static target striding: no late starters)
   int per_cu1 = 0, per_cu2 = 0;
-  XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, reinterpret_cast<const void*>(k1), 256, lds1));
+  XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, reinterpret_cast<const void*>(k1), thr1, lds1));
   XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, reinterpret_cast<const void*>(k2), 256, W.lds));
   per_cu1 = std::max(1, per_cu1);
   per_cu2 = std::max(1, per_cu2);
@@ -3107,7 +3288,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
     }
     a1.nr = nr;
     a1.row0 = r0;
-    hipLaunchKernelGGL(k1, dim3(g1), dim3(256), lds1, st, a1);
+    hipLaunchKernelGGL(k1, dim3(g1), dim3(thr1), lds1, st, a1);
     XPG_LAUNCHED();
     a2.nr = nr;
     a2.row0 = r0;

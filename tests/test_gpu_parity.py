@@ -29,14 +29,16 @@ def _eng():
     return engine
 
 
-@pytest.fixture(params=["rows", "fused", "unfused", "wide"])
+@pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
     32-samples-per-pass wide path for 2-layer plans (XPG_FORWARD=wide; default for frontiers of
     8192+ nodes) and the multi-kernel path (XPG_FORWARD=unfused, also the fallback for plans the
-    others do not take)."""
-    monkeypatch.setenv("XPG_FORWARD", request.param)
+    others do not take; "wide-mfma" = the wide path with its MFMA layer-1 kernel)."""
+    monkeypatch.setenv("XPG_FORWARD", request.param.split("-")[0])
+    if request.param == "wide-mfma":
+        monkeypatch.setenv("XPG_WIDE_L1", "mfma")
     return request.param
 
 
@@ -447,5 +449,5 @@ def test_c2_scale_forward_properties(fwd_path):
         try:
             y3 = plan.forward(bits)[:, 0]
         finally:
-            os.environ["XPG_FORWARD"] = fwd_path
+            os.environ["XPG_FORWARD"] = fwd_path.split("-")[0]
         torch.testing.assert_close(y3, y, rtol=0, atol=2e-6)
