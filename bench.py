@@ -124,6 +124,24 @@ def pmc_traffic(kernels, args):
                                     "summed over the chain's kernels)" if hit else None)
 
 
+def pmc_traffic_counts(counts):
+    """HBM bytes of one operation = sum over kernels of (dispatches per operation) x (measured
+    bytes per dispatch) from profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE of this bench's
+    default run, tools/pmc_traffic.py), or None when a kernel is missing."""
+    fn = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(fn):
+        return None
+    data = json.load(open(fn))
+    tot = 0.0
+    for prefix, n in counts.items():
+        hits = [d["traffic_bytes"] for name, d in data.items()
+                if name.startswith(prefix) and d.get("traffic_bytes") is not None]
+        if not hits:
+            return None
+        tot += n * sum(hits) / len(hits)
+    return tot
+
+
 def cpu_baseline(args, arch, sub_feat, sub_ei, q):
     """The numpy oracle (CPU restatement of the reference path, 1 thread) on a bounded sample
     of the same workload: cpu_rows mask rows through forward + KernelSHAP + surrogate."""
@@ -209,6 +227,10 @@ def full_graph_section(args, dev):
     bytes_ = full_graph_bytes(N, kept, E, 128, 128, rows)
     flops = rows * N * 2.0 * (2 * 128 * 128 + 128)  # layer-2 dense (l and r) + head, per target
     achieved = bytes_ / (ms * 1e-3) / 1e9
+    passes = -(-rows // 32)
+    traffic = pmc_traffic_counts({"k_wide_bits": passes, "k_wide_f0": passes,
+                                  "k_wide_degree": passes, "k_wide_tgt<8, false": passes,
+                                  "k_wide_tgt<8, true": passes}) if rows == 64 else None
     out = {
         "workload": "c3 full-graph masked forward (SURVEY.md §8d regime (ii)): 1M nodes / 10M "
                     "edges, 128 feats, 2-layer SAGEConv(mean) + Linear(128,1) + sigmoid, every "
@@ -220,6 +242,8 @@ def full_graph_section(args, dev):
                                "k_wide_tgt<layer 2 + head>)",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": bytes_,
+                     "traffic": traffic,
+                     "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
                      "bytes_formula": "SURVEY.md §8d B_alg per sample, E_kept measured per row"},
         "mfma": {"tflops": flops / (ms * 1e-3) / 1e12, "peak_fp32_tflops": 157.3,
                  "frac": flops / (ms * 1e-3) / 1e12 / 157.3},
@@ -306,6 +330,8 @@ def graph_prediction_section(args, dev):
     total = sum(ph.values())
     W = (N + 31) // 32
     wbytes = 2 * R * W * 4 + epochs * 6 * N * 4  # mask bits twice per step + Adam state r/w
+    traffic = pmc_traffic_counts({"k_gw_p": epochs, "k_gw_g": epochs, "k_gw_grad": epochs,
+                                  "k_gw_loss": 1})
     return {"workload": "c3 graph_prediction, one query (node 7), S = 1M mask columns, "
                         "interpret_samples=512 x epochs=50 = 25,600 rows, one repeat",
             "ms_per_repeat": total, "samples_per_s": R / (total * 1e-3), "phases_ms": ph,
@@ -314,7 +340,8 @@ def graph_prediction_section(args, dev):
                          "achieved": wbytes / (ph["wlm"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s",
                          "frac": wbytes / (ph["wlm"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "bytes_per_launch": wbytes,
+                         "bytes_per_launch": wbytes, "traffic": traffic,
+                         "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
                          "bytes_formula": "2 x R x ceil(S/32) x 4 (bits, p and grad passes) + "
                                           "steps x 24 S (w, m, v read + write)"},
             "sampler_GBps": R * W * 4 / (ph["sample"] * 1e-3) / 1e9}
