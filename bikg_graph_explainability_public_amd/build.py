@@ -19,7 +19,8 @@ def hipcc():
 
 
 def build(force=False, verbose=True):
-    deps = [SRC, os.path.join(os.path.dirname(HERE), "include", "xpgnn.h")]
+    deps = [SRC, os.path.join(HERE, "csrc", "khop.hip"),
+            os.path.join(os.path.dirname(HERE), "include", "xpgnn.h")]
     if not force and os.path.exists(OUT) and \
             all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT

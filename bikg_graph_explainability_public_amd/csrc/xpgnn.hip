@@ -3922,3 +3922,5 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
 }
 
 }  // extern "C"
+
+#include "khop.hip"

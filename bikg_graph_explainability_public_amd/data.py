@@ -1,8 +1,9 @@
 """Graph data utilities: the reference's `Data` class (data.py:19-878), same names and outputs.
 
 * Heterogeneous <-> homogeneous layout (data.py:39-232, 695-878) and names: host torch ops.
-* `comp_graph` (data.py:281-361): PyG-2.0.4 k_hop_subgraph semantics (L+1 hops, relabel) with
-  torch ops on the graph's device.
+* `comp_graph` (data.py:281-361): PyG-2.0.4 k_hop_subgraph semantics (L+1 hops, relabel).  On a
+  device graph (the Explainer.run path) it is the HIP frontier/compaction kernels
+  (`engine.khop_subgraph`, §8f1); a host graph (Data used on CPU tensors) uses torch ops.
 * Perturbation seams (`build_edge_mask`, `perturb_node`, `perturbator`, data.py:390-648): the
   edge keep test runs in the HIP kernel `xpg_edge_keep` on bit-packed masks (device tensors
   only; no CPU fallback).  The engine path never materialises the B-fold union graph at all.
@@ -22,9 +23,11 @@ def k_hop_subgraph(node_idx, num_hops, edge_index, num_nodes=None):
     edges num_hops times from the seed; subset = sorted unique visited nodes; keep every edge
     with both ends in subset (original order); relabel.  Returns (subset, edge_index, inv,
     edge_mask)."""
-    src, dst = edge_index[0], edge_index[1]
     if num_nodes is None:
         num_nodes = int(edge_index.max()) + 1 if edge_index.numel() else 1
+    if edge_index.device.type == "cuda":
+        return engine.khop_subgraph(int(node_idx), num_hops, edge_index, num_nodes)
+    src, dst = edge_index[0], edge_index[1]
     dev = edge_index.device
     seed = torch.tensor([int(node_idx)], device=dev)
     visited = [seed]

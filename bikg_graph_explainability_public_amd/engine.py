@@ -78,6 +78,33 @@ def edge_keep(bits, cols, src, dst):
     return keep.view(torch.bool)
 
 
+# ----------------------------------------------------------------------------- k-hop subgraph
+def khop_subgraph(node_idx: int, num_hops: int, edge_index: torch.Tensor, num_nodes: int):
+    """Data.comp_graph's k_hop_subgraph (data.py:331-333; PyG 2.0.4 semantics, relabel_nodes=True,
+    flow='source_to_target') on device: (subset int64, relabelled edge_index int64 [2, E_sub],
+    inv int64 [1], edge_mask bool [E]).  One host sync (the output sizes)."""
+    _lib.require_device(edge_index, "edge_index")
+    dev = edge_index.device
+    ei = edge_index.to(torch.int64).contiguous()
+    E, N, seed = ei.shape[1], int(num_nodes), int(node_idx)
+    if not 0 <= seed < N:
+        raise IndexError(f"k_hop_subgraph: node {seed} out of range for {N} nodes")
+    nbytes = ctypes.c_size_t(0)
+    call("xpg_khop_workspace", N, E, ctypes.byref(nbytes))
+    ws = _workspace(dev, nbytes.value)
+    subset = torch.empty(N, dtype=torch.int64, device=dev)
+    sub = torch.empty((2, max(E, 1)), dtype=torch.int64, device=dev)
+    emask = torch.empty(E, dtype=torch.uint8, device=dev)
+    counts = torch.empty(4, dtype=torch.int64, device=dev)
+    call("xpg_khop_subgraph", ptr(ei), E, N, seed, int(num_hops), ptr(subset), ptr(sub),
+         ptr(sub[1]), ptr(emask), ptr(counts), ptr(ws), ws.numel(), _lib.stream_of(dev))
+    n_sub, n_e, inv, bad = counts.tolist()
+    if bad:
+        raise IndexError("k_hop_subgraph: edge_index holds node ids outside [0, num_nodes)")
+    return (subset[:n_sub], sub[:, :n_e].contiguous(), torch.tensor([inv], dtype=torch.int64, device=dev),
+            emask.view(torch.bool))
+
+
 # ----------------------------------------------------------------------------- KernelSHAP
 def shap_kernel(bits: torch.Tensor, cols: int, counts: torch.Tensor = None) -> torch.Tensor:
     """Kernel.compute (kernels.py:115-174) on device: fp64 [rows].  `counts` (row popcounts from

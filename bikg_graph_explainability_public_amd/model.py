@@ -70,6 +70,57 @@ class Model:
             outs.append(out)
         return torch.tensor(outs, device=feat.device)
 
+    def predict_hetero_output_batched(self, feat, edge_index, node_types, edge_types,
+                                      node_type_names, edge_type_names, num_perturbs, num_nodes,
+                                      sub_ind=None, padded_dims=None, problem="node_prediction"):
+        """predict_hetero_output (model.py:118-253) with ONE `arch` call instead of one per copy
+        (SURVEY.md §8f2): the B copies become a disjoint union per node type — copy b's nodes of
+        type t are rows [b*n_t, (b+1)*n_t) of x_dict[t], relation edges are re-based the same
+        way — so every node-wise message-passing layer (GCN/SAGE/GAT, HeteroConv, Linear)
+        computes exactly the per-copy outputs.  Copies without edges give 0 as in the reference.
+        Returns None when the layout is not the contiguous per-type blocks the reference's
+        pointer arithmetic assumes (callers then use the per-copy loop)."""
+        if "node" not in problem or sub_ind is None:
+            return None
+        B, S = int(num_perturbs), int(num_nodes)
+        dev = feat.device
+        nt = node_types[:S]
+        uniq = torch.unique(node_types)
+        pointers = [int(torch.where(node_types == u)[0][0]) for u in uniq]
+        f3 = feat.reshape(B, S, feat.shape[1])
+        x_dict, n_of = {}, {}
+        for i, name in enumerate(node_type_names):
+            idx = torch.where(nt == i)[0]
+            n_of[name] = int(idx.numel())
+            if idx.numel() and int(idx[-1] - idx[0]) + 1 != idx.numel():
+                return None  # type rows not one contiguous block
+            block = f3[:, idx, :].reshape(B * idx.numel(), feat.shape[1])
+            if padded_dims is not None and padded_dims[i] > 0:
+                block = block[:, :-padded_dims[i]]
+            x_dict[name] = block
+        ei = edge_index.long()
+        copy = torch.div(ei[0], S, rounding_mode="floor")
+        e_dict = {}
+        for k, et in enumerate(edge_type_names):
+            sel = torch.where(edge_types == k)[0]
+            b = copy[sel]
+            out_e = []
+            for row, tname in ((0, et[0]), (1, et[-1])):
+                p = pointers[node_type_names.index(tname)]
+                loc = ei[row, sel] - b * S - p
+                if loc.numel() and (int(loc.min()) < 0 or int(loc.max()) >= n_of[tname]):
+                    return None
+                out_e.append(b * n_of[tname] + loc)
+            e_dict[et] = torch.stack(out_e) if sel.numel() else \
+                torch.zeros((2, 0), dtype=torch.long, device=dev)
+        with torch.no_grad():
+            out = self.arch(x_dict, e_dict)
+        if out.shape[0] % B:
+            return None
+        y = out.reshape(B, out.shape[0] // B, -1)[:, sub_ind, 0]
+        has_edges = torch.bincount(copy, minlength=B)[:B] > 0
+        return torch.where(has_edges, y, torch.zeros_like(y))
+
     @staticmethod
     def hetero2homo_output(hetero_output):
         """model.py:256-292."""

@@ -1,4 +1,4 @@
-"""PyG-2.0.4-compatible graph layers (GCNConv, SAGEConv, HeteroConv, Linear).
+"""PyG-2.0.4-compatible graph layers (GCNConv, SAGEConv, GATConv, HeteroConv, Linear).
 
 PyTorch Geometric is not available on ROCm boxes here; these modules carry the same
 `state_dict` keys as torch_geometric 2.0.4 (`lin.weight` / `bias` for GCNConv, `lin_l.*` /
@@ -24,24 +24,51 @@ def _uniform_(t, bound):
 
 
 class Linear(nn.Module):
+    """PyG Linear; in_channels <= 0 is lazy (shape taken from the first input or checkpoint)."""
+
     def __init__(self, in_channels, out_channels, bias=True, weight_initializer=None,
                  bias_initializer=None):
         super().__init__()
         self.in_channels, self.out_channels = in_channels, out_channels
-        self.weight = nn.Parameter(torch.empty(out_channels, in_channels))
-        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
-        if weight_initializer == "glorot":
-            _uniform_(self.weight, math.sqrt(6.0 / (in_channels + out_channels)))
+        self.weight_initializer, self.bias_initializer = weight_initializer, bias_initializer
+        if in_channels > 0:
+            self.weight = nn.Parameter(torch.empty(out_channels, in_channels))
         else:
-            _uniform_(self.weight, 1.0 / math.sqrt(max(in_channels, 1)))
+            self.weight = nn.parameter.UninitializedParameter()
+        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        if in_channels > 0:
+            self.reset_parameters()
+        elif self.bias is not None:
+            with torch.no_grad():
+                self.bias.zero_()
+
+    def reset_parameters(self):
+        fan_in = self.weight.shape[1]
+        if self.weight_initializer == "glorot":
+            _uniform_(self.weight, math.sqrt(6.0 / (fan_in + self.out_channels)))
+        else:
+            _uniform_(self.weight, 1.0 / math.sqrt(max(fan_in, 1)))
         if self.bias is not None:
-            if bias_initializer == "zeros":
+            if self.bias_initializer == "zeros":
                 with torch.no_grad():
                     self.bias.zero_()
             else:
-                _uniform_(self.bias, 1.0 / math.sqrt(max(in_channels, 1)))
+                _uniform_(self.bias, 1.0 / math.sqrt(max(fan_in, 1)))
+
+    def _materialize(self, in_channels, device, dtype):
+        if isinstance(self.weight, nn.parameter.UninitializedParameter):
+            self.weight.materialize((self.out_channels, in_channels), device=device, dtype=dtype)
+            self.in_channels = in_channels
+            self.reset_parameters()
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        w = state_dict.get(prefix + "weight")
+        if w is not None:
+            self._materialize(w.shape[1], w.device, w.dtype)
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
     def forward(self, x):
+        self._materialize(x.shape[-1], x.device, x.dtype)
         return F.linear(x, self.weight, self.bias)
 
     def extra_repr(self):
@@ -112,6 +139,67 @@ class SAGEConv(MessagePassing):
 
     def extra_repr(self):
         return f"{self.in_channels}, {self.out_channels}, aggr={self.aggr}"
+
+
+class GATConv(MessagePassing):
+    """GATConv (PyG 2.0.4): h = x W (W_src / W_dst for bipartite inputs), attention
+    softmax over each target's in-edges of leaky_relu(a_src . h_j + a_dst . h_i, 0.2), heads
+    concatenated (or averaged), + bias.  The conv of the reference's multi-node-type test arch
+    (tests/test_utils.py:86-182: HeteroConv of GATConv((-1, -1), c, add_self_loops=False)).
+    The engine does not compile it: archs using it run on the generic (batched) path."""
+
+    def __init__(self, in_channels, out_channels, heads=1, concat=True, negative_slope=0.2,
+                 dropout=0.0, add_self_loops=True, bias=True, **kwargs):
+        super().__init__()
+        self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
+        self.concat, self.negative_slope, self.dropout = concat, negative_slope, dropout
+        self.add_self_loops = add_self_loops
+        if isinstance(in_channels, int):
+            self.lin_src = Linear(in_channels, heads * out_channels, bias=False,
+                                  weight_initializer="glorot")
+            self.lin_dst = self.lin_src
+        else:
+            self.lin_src = Linear(in_channels[0], heads * out_channels, bias=False,
+                                  weight_initializer="glorot")
+            self.lin_dst = Linear(in_channels[1], heads * out_channels, bias=False,
+                                  weight_initializer="glorot")
+        self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
+        _uniform_(self.att_src, math.sqrt(6.0 / (heads + out_channels)))
+        _uniform_(self.att_dst, math.sqrt(6.0 / (heads + out_channels)))
+        n_bias = heads * out_channels if concat else out_channels
+        self.bias = nn.Parameter(torch.zeros(n_bias)) if bias else None
+
+    def forward(self, x, edge_index):
+        H, C = self.heads, self.out_channels
+        xs, xd = (x, x) if isinstance(x, torch.Tensor) else x
+        hs = self.lin_src(xs).view(-1, H, C)
+        hd = hs if (xd is xs and self.lin_dst is self.lin_src) else self.lin_dst(xd).view(-1, H, C)
+        a_s = (hs * self.att_src).sum(-1)
+        a_d = (hd * self.att_dst).sum(-1)
+        ei = edge_index.long()
+        n = hd.size(0)
+        if self.add_self_loops:
+            loop = torch.arange(min(hs.size(0), n), device=ei.device)
+            ei = torch.cat([ei[:, ei[0] != ei[1]], torch.stack([loop, loop])], 1)
+        src, dst = ei[0], ei[1]
+        alpha = F.leaky_relu(a_s[src] + a_d[dst], self.negative_slope)          # [E, H]
+        idx = dst.unsqueeze(1).expand(-1, H)
+        amax = torch.zeros((n, H), dtype=alpha.dtype, device=alpha.device).scatter_reduce(
+            0, idx, alpha, reduce="amax", include_self=False)
+        ex = (alpha - amax[dst]).exp()
+        den = torch.zeros((n, H), dtype=alpha.dtype, device=alpha.device).index_add_(0, dst, ex)
+        alpha = ex / (den[dst] + 1e-16)
+        alpha = F.dropout(alpha, p=self.dropout, training=self.training)
+        out = torch.zeros((n, H, C), dtype=hs.dtype, device=hs.device)
+        out.index_add_(0, dst, hs[src] * alpha.unsqueeze(-1))
+        out = out.reshape(n, H * C) if self.concat else out.mean(dim=1)
+        if self.bias is not None:
+            out = out + self.bias
+        return out
+
+    def extra_repr(self):
+        return f"{self.in_channels}, {self.out_channels}, heads={self.heads}"
 
 
 class HeteroConv(nn.Module):

@@ -9,6 +9,7 @@ Architectures the engine cannot compile run through `generic_outputs` (the user'
 on the B-fold union graph built with the HIP edge-keep kernel) — still on the GPU, with the
 KernelSHAP and surrogate stages unchanged.
 """
+import os
 import warnings
 
 import torch
@@ -74,8 +75,17 @@ def generic_outputs(arch, feat, edge_index, mask, element_index, problem, node_t
         if n_types < 2:
             out = mc.infer(cf, pei, cnt, pet)
         else:
-            out = mc.predict_hetero_output(cf, pei, cnt, pet, node_type_names, edge_type_names,
-                                           B, S, element_index, padded_dims, problem)
+            # one arch call over the disjoint union per node type (§8f2); XPG_HETERO_LOOP=1
+            # restores the reference's per-copy loop
+            out = None
+            if os.environ.get("XPG_HETERO_LOOP", "0") != "1":
+                out = mc.predict_hetero_output_batched(cf, pei, cnt, pet, node_type_names,
+                                                       edge_type_names, B, S, element_index,
+                                                       padded_dims, problem)
+            if out is None:
+                out = mc.predict_hetero_output(cf, pei, cnt, pet, node_type_names,
+                                               edge_type_names, B, S, element_index,
+                                               padded_dims, problem)
         if node_type is not None and edge_type is not None and isinstance(out, dict):
             out, _ = mc.hetero2homo_output(out)
         if element_index is not None:

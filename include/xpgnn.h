@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 5
+#define XPG_ABI_VERSION 6
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -163,6 +163,21 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
                 const xpg_wlm_params* params, int64_t step0, float* w, float* adam_m,
                 float* adam_v, double* losses, int32_t* best_epoch, void* workspace,
                 size_t workspace_bytes, xpg_stream_t stream);
+
+/* ---------------------------------------------------------------- k-hop computational subgraph */
+/* Replaces Data.comp_graph's PyG k_hop_subgraph(seed, hops, edge_index, relabel_nodes=True,
+ * flow='source_to_target') call (reference data.py:331-333).  Workspace for a graph of
+ * n_nodes nodes and n_edges edges. */
+int xpg_khop_workspace(int64_t n_nodes, int64_t n_edges, size_t* bytes);
+/* edge_index: int64 [2][n_edges] (row 0 = source, row 1 = target).  Outputs (device):
+ * subset [n_nodes capacity] sorted node ids; sub_src / sub_dst [n_edges capacity] relabelled
+ * kept edges in original order; edge_mask [n_edges] (0/1 bytes); counts [4] =
+ * {|subset|, kept edges, position of seed in subset, 1 if any edge id was out of range}.
+ * Asynchronous: the caller reads counts after synchronising the stream. */
+int xpg_khop_subgraph(const int64_t* edge_index, int64_t n_edges, int64_t n_nodes, int64_t seed,
+                      int32_t hops, int64_t* subset, int64_t* sub_src, int64_t* sub_dst,
+                      uint8_t* edge_mask, int64_t* counts, void* workspace,
+                      size_t workspace_bytes, xpg_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -451,3 +451,82 @@ def test_c2_scale_forward_properties(fwd_path):
         finally:
             os.environ["XPG_FORWARD"] = fwd_path.split("-")[0]
         torch.testing.assert_close(y3, y, rtol=0, atol=2e-6)
+
+
+# ------------------------------------------------------------------ k-hop subgraph (§8f1)
+def _khop_check(ei, n, seed, hops):
+    e = _eng()
+    subset, sub_ei, inv, emask = e.khop_subgraph(seed, hops, torch.as_tensor(ei).to(DEV), n)
+    o_subset, o_sub_ei, o_inv, o_emask = oracle.k_hop_subgraph(seed, hops, ei, n)
+    np.testing.assert_array_equal(subset.cpu().numpy(), o_subset)
+    np.testing.assert_array_equal(sub_ei.cpu().numpy().reshape(2, -1), o_sub_ei.reshape(2, -1))
+    assert int(inv[0]) == o_inv
+    np.testing.assert_array_equal(emask.cpu().numpy(), o_emask)
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("hops", [0, 1, 2, 3, 4])
+def test_khop_vs_oracle_golden_graphs(name, hops):
+    """The reference graphs of the golden cases (their comp_graph is what pins the oracle's
+    subset size: the mask width S of every recorded mask)."""
+    from test_oracle_golden import homogenize
+    from golden_utils import case_inputs
+    z, meta = load_case(name)
+    x, ei, _, _ = homogenize(*case_inputs(z))
+    for seed in sorted({0, x.shape[0] // 2, x.shape[0] - 1}):
+        _khop_check(np.asarray(ei, dtype=np.int64), x.shape[0], seed, hops)
+
+
+@pytest.mark.parametrize("N,E,hops", [(1, 0, 3), (5, 0, 2), (50, 400, 3), (4097, 9000, 2),
+                                      (20000, 8191, 4), (100000, 1000000, 3)])
+def test_khop_vs_oracle_random(N, E, hops):
+    """Random graphs with self-loops and duplicate edges; block-boundary sizes (4096 items per
+    block); isolated seeds; empty edge sets."""
+    g = np.random.default_rng(N * 7 + E)
+    ei = g.integers(0, N, size=(2, E), dtype=np.int64)
+    if E:
+        d = E // 50
+        ei[:, :d] = ei[0, :d]                        # self-loops
+        ei[:, d:2 * d] = ei[:, :d]                   # duplicates
+    for seed in sorted({0, N // 3, N - 1}):
+        _khop_check(ei, N, seed, hops)
+
+
+def test_khop_full_size_properties():
+    """c3 graph size (1M nodes, 10M edges): subset sorted unique and contains the seed; every
+    kept edge lies inside the subset and every edge inside it is kept; relabel is a bijection."""
+    e = _eng()
+    N, E, seed = 1_000_000, 10_000_000, 7
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    ei = torch.randint(0, N, (2, E), device=DEV, generator=gen)
+    subset, sub_ei, inv, emask = e.khop_subgraph(seed, 3, ei, N)
+    assert bool((subset[1:] > subset[:-1]).all()) and int(subset[inv[0]]) == seed
+    inset = torch.zeros(N, dtype=torch.bool, device=DEV)
+    inset[subset] = True
+    assert torch.equal(emask, inset[ei[0]] & inset[ei[1]])
+    assert torch.equal(subset[sub_ei], ei[:, emask])
+    o = oracle.k_hop_subgraph(seed, 3, ei.cpu().numpy(), N)
+    np.testing.assert_array_equal(subset.cpu().numpy(), o[0])
+
+
+def test_khop_rejects_bad_ids():
+    e = _eng()
+    ei = torch.tensor([[0, 1, 9], [1, 2, 0]], device=DEV)
+    with pytest.raises(IndexError):
+        e.khop_subgraph(0, 2, ei, 3)
+    with pytest.raises(IndexError):
+        e.khop_subgraph(5, 2, ei[:, :2], 3)
+
+
+def test_comp_graph_device_matches_host():
+    """Data.comp_graph on a device graph (HIP k-hop) equals the host-tensor path."""
+    from bikg_graph_explainability_public_amd.data import Data
+    g = torch.Generator().manual_seed(11)
+    feat = torch.randn(300, 8, generator=g)
+    ei = torch.randint(0, 300, (2, 1500), generator=g)
+    names = [str(i) for i in range(300)]
+    for q in (0, 17, 299):
+        a = Data(feat, ei).comp_graph(q, 2, "node_prediction", names)
+        b = Data(feat.to(DEV), ei.to(DEV)).comp_graph(q, 2, "node_prediction", names)
+        assert torch.equal(a[0], b[0].cpu()) and torch.equal(a[1], b[1].cpu())
+        assert a[2] == b[2] and int(a[3]) == int(b[3])
