@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -25,7 +25,7 @@ class NativeLibraryError(RuntimeError):
 
 
 class TermDesc(ctypes.Structure):
-    _fields_ = [("kind", c_i32), ("rel", c_i32), ("table", c_vp)]
+    _fields_ = [("kind", c_i32), ("rel", c_i32), ("table", c_vp), ("dst_type", c_i32)]
 
 
 class LayerDesc(ctypes.Structure):
@@ -33,7 +33,8 @@ class LayerDesc(ctypes.Structure):
                 ("f_out_pad", c_i32), ("n_tgt", c_i32), ("n_edges", c_i32), ("tgt_prev", c_vp),
                 ("tgt_f0", c_vp),
                 ("agg_ptr", c_vp), ("agg_src", c_vp), ("agg_f0", c_vp), ("self_mult", c_vp),
-                ("terms", TermDesc * MAX_TERMS), ("weight", c_vp), ("bias", c_vp)]
+                ("terms", TermDesc * MAX_TERMS), ("weight", c_vp), ("bias", c_vp),
+                ("tgt_type", c_vp), ("n_types", c_i32)]
 
 
 class HeadDesc(ctypes.Structure):

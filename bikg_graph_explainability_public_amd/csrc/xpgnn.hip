@@ -300,7 +300,9 @@ template <int NT>
 __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int64_t M, int64_t lda,
                                                const float* __restrict__ W, int64_t ldw, int k_pad,
                                                const float* __restrict__ bias, int n_real, int act,
-                                               float* __restrict__ C, int64_t ldc) {
+                                               float* __restrict__ C, int64_t ldc,
+                                               const int32_t* __restrict__ row_type, int64_t type_mod,
+                                               int bias_ld) {
   const int lane = threadIdx.x & 63;
   const int64_t m0 = (blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 32;
   if (m0 >= M) return;
@@ -331,7 +333,9 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int64_t m = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      if (m < M) C[m * ldc + col] = col < n_real ? act_apply(acc[nt][reg] + bv, act) : 0.f;
+      // multi-node-type layers: the bias of the row's target type (rows are (mask row, target))
+      const float b = (row_type && m < M && col < n_real) ? bias[(int64_t)row_type[m % type_mod] * bias_ld + col] : bv;
+      if (m < M) C[m * ldc + col] = col < n_real ? act_apply(acc[nt][reg] + b, act) : 0.f;
     }
   }
 }
@@ -379,9 +383,11 @@ struct AggArgs {
   int width;            // source row width (floats, % 32 == 0)
   float* out;
   int64_t out_ld;
-  const float* bias;    // layer 1 epilogue
+  const float* bias;    // layer 1 epilogue ([n_types][width] with tgt_type)
   int act;
   int f_real;
+  const int32_t* tgt_type;      // multi-node-type plans: node type of each target (else null)
+  int dst_type[XPG_MAX_TERMS];  // term k reaches only targets of this type (-1: every target)
 };
 
 __device__ __forceinline__ float inv_sqrt_deg(float kin) {
@@ -424,7 +430,10 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
     float4 s[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) s[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (kind == XPG_TERM_ROOT) {
+    // HeteroConv on several node types: a relation's conv only produces rows of its
+    // destination type (hetero_conv.py sums per destination), so other targets get 0
+    if (a.tgt_type && a.dst_type[k] >= 0 && a.tgt_type[t] != a.dst_type[k]) {
+    } else if (kind == XPG_TERM_ROOT) {
 #pragma unroll
       for (int j = 0; j < NV; ++j) s[j] = selfrow[sub + j * LPS];
     } else {
@@ -485,12 +494,13 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
   }
   if (L1) {
     float4* o = reinterpret_cast<float4*>(a.out + item * a.out_ld);
+    const float* bias = a.bias + (a.tgt_type ? (int64_t)a.tgt_type[t] * a.width : 0);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int f = (sub + j * LPS) * 4;
       float v[4] = {tot[j].x, tot[j].y, tot[j].z, tot[j].w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = (f + q < a.f_real) ? act_apply(v[q] + a.bias[f + q], a.act) : 0.f;
+      for (int q = 0; q < 4; ++q) v[q] = (f + q < a.f_real) ? act_apply(v[q] + bias[f + q], a.act) : 0.f;
       o[sub + j * LPS] = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
@@ -2888,6 +2898,13 @@ __global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t*
 // ------------------------------------------------------------------------------------ helpers
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
 
+// node-type-gated terms (multi-node-type HeteroConv) run on the multi-kernel path only
+bool plan_multi_type(const xpg_forward_plan* p) {
+  for (int l = 0; l < p->n_layers; ++l)
+    if (p->layers[l].tgt_type) return true;
+  return false;
+}
+
 struct WsLayout {
   size_t kin = 0, agg = 0, head0 = 0, head1 = 0, total = 0;
   size_t h[64];
@@ -2926,7 +2943,7 @@ int layout_ws(const xpg_forward_plan* p, int64_t rows, WsLayout* L) {
 
 int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t ldw, int64_t k_pad,
                  const float* bias, int64_t n_real, int64_t n_pad, int act, float* C, int64_t ldc,
-                 hipStream_t st) {
+                 hipStream_t st, const int32_t* row_type = nullptr, int64_t type_mod = 1, int bias_ld = 0) {
   XPG_REQ(k_pad % 8 == 0 && n_pad % 32 == 0 && n_pad >= 32 && n_pad <= 256,
           "xpg_dense: k_pad % 8, n_pad in {32..256} step 32 required");
   XPG_REQ(lda % 4 == 0 && ldw % 4 == 0, "xpg_dense: lda/ldw must be multiples of 4");
@@ -2936,7 +2953,8 @@ int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t
   const int kp = static_cast<int>(k_pad), nr = static_cast<int>(n_real);
   switch (n_pad / 32) {
 #define XPG_DENSE_CASE(NT) \
-    case NT: hipLaunchKernelGGL(k_dense<NT>, grid, block, 0, st, A, M, lda, W, ldw, kp, bias, nr, act, C, ldc); break;
+    case NT: hipLaunchKernelGGL(k_dense<NT>, grid, block, 0, st, A, M, lda, W, ldw, kp, bias, nr, act, C, ldc, \
+                                row_type, type_mod, bias_ld); break;
     XPG_DENSE_CASE(1) XPG_DENSE_CASE(2) XPG_DENSE_CASE(3) XPG_DENSE_CASE(4)
     XPG_DENSE_CASE(5) XPG_DENSE_CASE(6) XPG_DENSE_CASE(7) XPG_DENSE_CASE(8)
 #undef XPG_DENSE_CASE
@@ -2970,7 +2988,7 @@ int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t r
   // opt-in (XPG_FORWARD=fused): per-row latency chains make it slower than k_rows_forward
   const char* env = getenv("XPG_FORWARD");
   if (!env || std::strcmp(env, "fused") != 0) return 1;
-  if (p->n_layers > kFusedMaxLayers || p->n_head > kFusedMaxHead) return 1;
+  if (p->n_layers > kFusedMaxLayers || p->n_head > kFusedMaxHead || plan_multi_type(p)) return 1;
   FusedArgs a;
   std::memset(&a, 0, sizeof(a));
   a.rows = rows;
@@ -3095,7 +3113,7 @@ struct WideWs {
 };
 
 int wide_layout(const xpg_forward_plan* p, WideWs* W) {
-  if (p->n_layers != 2 || p->n_head > kFusedMaxHead || p->n_head < 0) return 1;
+  if (p->n_layers != 2 || p->n_head > kFusedMaxHead || p->n_head < 0 || plan_multi_type(p)) return 1;
   const xpg_layer_desc& l1 = p->layers[0];
   const xpg_layer_desc& l2 = p->layers[1];
   if (l1.n_terms < 1 || l1.n_terms > XPG_MAX_TERMS || l2.n_terms < 1 || l2.n_terms > XPG_MAX_TERMS) return 1;
@@ -3300,7 +3318,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
 
 // Lanes-=-rows fused forward for 1- and 2-layer plans (returns 1 when it does not apply).
 int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
-  if (p->n_layers < 1 || p->n_layers > 2 || p->n_head > kFusedMaxHead) return 1;
+  if (p->n_layers < 1 || p->n_layers > 2 || p->n_head > kFusedMaxHead || plan_multi_type(p)) return 1;
   RowsFwdArgs a;
   std::memset(&a, 0, sizeof(a));
   a.rows = rows;
@@ -3609,11 +3627,14 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
     a.agg_f0 = ly.agg_f0;
     a.self_mult = ly.self_mult;
     a.n_terms = ly.n_terms;
+    a.tgt_type = ly.tgt_type;
     for (int k = 0; k < ly.n_terms; ++k) {
       a.kind[k] = ly.terms[k].kind;
       a.rel[k] = ly.terms[k].rel;
       a.table[k] = ly.terms[k].table;
+      a.dst_type[k] = ly.tgt_type ? ly.terms[k].dst_type : -1;
       XPG_REQ(a.kind[k] == XPG_TERM_ROOT || (a.rel[k] >= 0 && a.rel[k] < p->n_rel), "term: bad relation");
+      XPG_REQ(!ly.tgt_type || a.dst_type[k] < ly.n_types, "term: destination type out of range");
     }
     float* hout = reinterpret_cast<float*>(ws + L.h[l]);
     if (l == 0) {
@@ -3636,7 +3657,7 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
       rc = launch_agg<false>(a, st);
       if (rc) return rc;
       rc = launch_dense(agg, rows * ly.n_tgt, a.out_ld, ly.weight, a.out_ld, a.out_ld, ly.bias, ly.f_out,
-                        ly.f_out_pad, ly.act, hout, ly.f_out_pad, st);
+                        ly.f_out_pad, ly.act, hout, ly.f_out_pad, st, ly.tgt_type, ly.n_tgt, ly.f_out_pad);
       if (rc) return rc;
     }
   }

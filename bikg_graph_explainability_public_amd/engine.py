@@ -209,7 +209,9 @@ def plan_arrays(S, rel_np, queries, L):
 class ForwardPlan:
     """Receptive-field plan of one (subgraph, model program, query set)."""
 
-    def __init__(self, program, sub_feat, rel_edges, queries, device=None):
+    def __init__(self, program, sub_feat, rel_edges, queries, device=None, node_type=None):
+        """`node_type` ([S] node type of every subgraph node) is required by multi-node-type
+        programs: per layer, every target's type gates the relation terms (xpgnn.h)."""
         device = torch.device(device) if device is not None else sub_feat.device
         _lib.require_device(torch.empty(0, device=device), "plan device")
         if len(program.convs) == 0:
@@ -236,6 +238,15 @@ class ForwardPlan:
 
         X0 = sub_feat.to(device=device, dtype=torch.float32)[torch.as_tensor(fr[0], device=device)]
         f_in0 = program.convs[0].f_in
+        nt_np = None
+        if program.n_types > 1:
+            if node_type is None:
+                raise ValueError("multi-node-type program needs the subgraph node types")
+            nt_np = np.asarray(torch.as_tensor(node_type).detach().cpu().numpy()).astype(np.int64)
+            if nt_np.shape != (S,) or nt_np.min() < 0 or nt_np.max() >= program.n_types:
+                raise ValueError("node types out of range")
+            if X0.shape[1] > f_in0:  # widest types are zero-padded beyond every relation's input
+                X0 = X0[:, :f_in0]
         if X0.shape[1] != f_in0:
             raise ValueError(f"feature width {X0.shape[1]} != first conv input {f_in0}")
 
@@ -262,13 +273,17 @@ class ForwardPlan:
             ld.agg_src = self._i32(lay["agg_src"] if lay["agg_src"].size else np.zeros(1)).data_ptr()
             ld.agg_f0 = self._i32(lay["agg_f0"] if lay["agg_f0"].size else np.zeros(1)).data_ptr()
             ld.self_mult = self._i32(lay["self_mult"]).data_ptr()
-            bias = torch.zeros(f_out_pad, dtype=torch.float32, device=device)
-            bias[:conv.f_out] = conv.bias.to(device)
+            n_types = program.n_types
+            bias = torch.zeros((n_types, f_out_pad), dtype=torch.float32, device=device)
+            bias[:, :conv.f_out] = conv.bias.to(device).reshape(-1, conv.f_out)
             self._keep.append(bias)
             ld.bias = bias.data_ptr()
+            ld.n_types = n_types
+            ld.tgt_type = self._i32(nt_np[fr[lvl]]).data_ptr() if nt_np is not None else None
             for k, term in enumerate(conv.terms):
                 ld.terms[k].kind = TERM[term.kind]
                 ld.terms[k].rel = term.rel
+                ld.terms[k].dst_type = term.dst_type
             if li == 0:
                 for k, term in enumerate(conv.terms):
                     T = dense(X0, term.weight.to(device), None, None)

@@ -224,15 +224,23 @@ class Explainer:
         # every rank returns the single-GPU result (sharding.py).
         flat = bits.reshape(times * R, -1)
         g = self.group
+        # multi-node-type graphs: the reference's per-copy loop zeroes copies without edges and
+        # its extraction re-cuts the [B] outputs (quirk Q4); params["hetero_q4"] = False keeps
+        # the per-copy outputs instead (model.py:118-253, wlm.py:435-436)
+        q4 = bool(self.params.get("hetero_q4", True))
         if plan is not None:
             y = sharding.gather_map(times * R, lambda s, e: plan.forward(flat[s:e])[:, 0],
                                     g).reshape(times, R)
+            if getattr(plan, "multi_type", False):
+                empty = pipeline.empty_copy_rows(flat, S, sub_ei).reshape(times, R)
+                y = torch.stack([pipeline.multi_type_targets(y[i], empty[i], batch, sub_ind, S, q4)
+                                 for i in range(times)])
         else:
             def generic(t0, t1):
                 ys = [pipeline.generic_outputs(
                     self.arch, sub_feat, sub_ei,
                     engine.unpack_masks(bits_list[i], S) if masks[i] is None else masks[i],
-                    sub_ind, self.problem, *geo, batch=batch) for i in range(t0, t1)]
+                    sub_ind, self.problem, *geo, batch=batch, q4=q4) for i in range(t0, t1)]
                 return torch.stack(ys) if ys else torch.empty((0, R), device=device)
             y = sharding.gather_map(times, generic, g)
 

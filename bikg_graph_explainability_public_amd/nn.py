@@ -264,3 +264,34 @@ class ConvStack(nn.Module):
         for layer in self.fc:
             x = layer(x)
         return x
+
+
+class HeteroSageStack(nn.Module):
+    """Multi-node-type model family: [HeteroConv({(src, rel, dst): SAGEConv}) -> ReLU]* then
+    Linear layers on the first output node type — the layout of the reference's multi-type
+    test arch (tests/test_utils.py:86-182) with SAGEConv relations (bipartite layer-1 inputs
+    (F_src, F_dst)).  state_dict keys: conv.<2l>.convs.<src>__<rel>__<dst>.lin_l/lin_r.*,
+    fc.<2i>.weight/bias."""
+
+    def __init__(self, rels, in_dims, hidden, n_layers, fc_dims):
+        super().__init__()
+        convs = []
+        for li in range(n_layers):
+            convs.append(HeteroConv({tuple(r): SAGEConv((in_dims[r[0]], in_dims[r[-1]])
+                                                        if li == 0 else (hidden, hidden), hidden)
+                                     for r in rels}))
+            convs.append(nn.ReLU())
+        self.conv = nn.ModuleList(convs)
+        fcs = []
+        for i in range(len(fc_dims) - 1):
+            fcs.append(Linear(fc_dims[i], fc_dims[i + 1]))
+            fcs.append(nn.Sigmoid() if i == len(fc_dims) - 2 else nn.ReLU())
+        self.fc = nn.ModuleList(fcs)
+
+    def forward(self, x, edge_index):
+        for i, c in enumerate(self.conv):
+            x = c(x, edge_index) if i % 2 == 0 else {k: c(v) for k, v in x.items()}
+        x = x[list(x.keys())[0]]
+        for layer in self.fc:
+            x = layer(x)
+        return x

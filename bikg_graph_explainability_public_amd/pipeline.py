@@ -29,31 +29,85 @@ def relation_edges(edge_index, edge_type, n_rel):
 
 def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
                node_type_names=None, edge_type_names=None, padded_dims=None):
-    """ForwardPlan for `arch` on the (sub)graph, or None when the engine cannot run it."""
-    if node_type_names is not None and node_type is not None and \
-            len(torch.unique(node_type)) >= 2:
-        return None  # multi-node-type graphs: per-copy generic path (model.py:118-253)
+    """ForwardPlan for `arch` on the (sub)graph, or None when the engine cannot run it.
+
+    Multi-node-type graphs (model.py:118-253): the program's terms are gated by destination
+    node type and the query is the reference's `out[sub_ind, 0]` — row sub_ind of the output
+    node type's block — so `queries` are positions inside that type and are mapped to subgraph
+    nodes here.  The plan is marked `multi_type` (its per-row outputs then go through
+    `multi_type_targets`)."""
+    multi = node_type_names is not None and node_type is not None and \
+        len(torch.unique(node_type)) >= 2
     hetero = edge_type_names is not None and edge_type is not None
     try:
-        prog = compile_arch(arch, edge_type_names if hetero else None)
+        prog = compile_arch(arch, edge_type_names if hetero else None,
+                            node_type_names if multi else None)
     except UnsupportedArch as e:
         warnings.warn(f"engine cannot compile arch ({e}); using the generic torch path")
         return None
     x = feat
-    if hetero and padded_dims is not None and padded_dims[0] > 0:
+    nt = None
+    if multi:
+        nt = node_type.long().reshape(-1)
+        rows_t = torch.where(nt == prog.out_type)[0].cpu()
+        queries = [int(q) for q in queries]
+        if any(q >= rows_t.numel() for q in queries):
+            raise IndexError("query index beyond the output node type's rows (model.py:247)")
+        queries = [int(rows_t[q]) for q in queries]
+    elif hetero and padded_dims is not None and padded_dims[0] > 0:
         x = feat[:, :feat.shape[1] - padded_dims[0]]
     rels = relation_edges(edge_index, edge_type if hetero else None,
                           len(edge_type_names) if hetero else 1)
     try:
-        return engine.ForwardPlan(prog, x, rels, queries)
+        plan = engine.ForwardPlan(prog, x, rels, queries, node_type=nt)
     except ValueError as e:
         warnings.warn(f"engine plan rejected ({e}); using the generic torch path")
         return None
+    plan.multi_type = multi
+    return plan
+
+
+def empty_copy_rows(bits, cols, edge_index, max_bytes=256 << 20):
+    """bool [rows]: mask rows that keep no edge of the (sub)graph — the reference's
+    multi-node-type loop outputs 0 for such copies instead of running the model
+    (model.py:213-215).  Uses the HIP edge-keep kernel in row chunks."""
+    rows, E = bits.shape[0], edge_index.shape[1]
+    out = torch.ones(rows, dtype=torch.bool, device=bits.device)
+    if E == 0:
+        return out
+    step = max(1, max_bytes // E)
+    for r0 in range(0, rows, step):
+        keep = engine.edge_keep(bits[r0:r0 + step], cols, edge_index[0], edge_index[1])
+        out[r0:r0 + step] = ~keep.view(-1, E).any(1)
+    return out
+
+
+def multi_type_targets(y_rows, empty, batch, sub_ind, S, q4=True):
+    """Regression targets of a multi-node-type repeat from per-row engine outputs.
+    Copies without edges give 0 (model.py:213-215).  With q4 (the reference's behaviour,
+    SURVEY.md quirk Q4) each batch's [B] outputs are cut again by
+    extract_node_edge_output(out, sub_ind, S) (wlm.py:435-436): the one surviving value is
+    the target of every row of the batch; q4=False keeps the per-copy outputs."""
+    y = torch.where(empty, torch.zeros_like(y_rows), y_rows)
+    if not q4:
+        return y
+    out = torch.empty_like(y)
+    for r0 in range(0, y.shape[0], batch):
+        yb = y[r0:r0 + batch]
+        sel = yb[sub_ind::S]
+        if sel.numel() == yb.numel():
+            out[r0:r0 + batch] = sel
+        elif sel.numel() == 1:
+            out[r0:r0 + batch] = sel.expand(yb.numel())
+        else:
+            raise RuntimeError("model output does not broadcast against the mask batch "
+                               "(the reference's weighted_mse_loss would fail here too)")
+    return out
 
 
 def generic_outputs(arch, feat, edge_index, mask, element_index, problem, node_type=None,
                     edge_type=None, node_type_names=None, edge_type_names=None,
-                    padded_dims=None, batch=None):
+                    padded_dims=None, batch=None, q4=True):
     """wlm.py:349-436 semantics per batch of mask rows with the user's module in torch.
     Returns y [R] (the regression target of each row; for multi-node-type graphs the
     reference's output[ind::S] collapse, quirk Q4, broadcast over its batch)."""
@@ -88,7 +142,7 @@ def generic_outputs(arch, feat, edge_index, mask, element_index, problem, node_t
                                                padded_dims, problem)
         if node_type is not None and edge_type is not None and isinstance(out, dict):
             out, _ = mc.hetero2homo_output(out)
-        if element_index is not None:
+        if element_index is not None and (q4 or n_types < 2):
             out = mc.extract_node_edge_output(out, element_index, S)
         out = out.reshape(-1).float()
         if out.numel() == B:
@@ -109,9 +163,13 @@ def verify_plan(plan, arch, feat, edge_index, query, node_type=None, edge_type=N
     S = feat.shape[0]
     mask = (torch.rand((rows, S), generator=g) < 0.5).to(feat.device)
     mask[0] = True
+    multi = getattr(plan, "multi_type", False)
     ref = generic_outputs(arch, feat, edge_index, mask, query, "node", node_type, edge_type,
-                          node_type_names, edge_type_names, padded_dims)
-    got = plan.forward(engine.pack_masks(mask))[:, 0]
+                          node_type_names, edge_type_names, padded_dims, q4=not multi)
+    bits = engine.pack_masks(mask)
+    got = plan.forward(bits)[:, 0]
+    if multi:  # per-copy outputs on both sides (zero for copies without edges)
+        got = torch.where(empty_copy_rows(bits, S, edge_index), torch.zeros_like(got), got)
     err = (ref - got).abs().max().item()
     return err <= tol * max(1.0, ref.abs().max().item()), err
 

@@ -9,6 +9,13 @@ tests/test_utils.py:10-83 and the notebooks) — and lowers it to:
     ConvLayer(terms=[(kind, relation, W_k)], bias_sum, act)   per conv layer
     HeadLayer(W, b, act)                                       per Linear
 
+Multi-node-type graphs (HeteroConv over relations (src, rel, dst) between several node types,
+model.py:118-253): every term carries its relation's destination type (the engine applies it
+only to targets of that type), SAGE root weights and biases are summed per destination type,
+and layer-1 weights are zero-padded to the widest input (the homogenised features are padded the
+same way, data.py:825-878).  The head reads the first output node type of the last HeteroConv
+(the `x[list(x.keys())[0]]` convention of the reference's hetero archs, tests/test_utils.py:176-178).
+
 Modules are matched by class name + attributes, so both torch_geometric 2.0.4 modules and
 bikg_graph_explainability_public_amd.nn modules compile.  Anything else raises
 UnsupportedArch (callers then use the generic torch path, model.py).
@@ -29,12 +36,13 @@ class Term:
     kind: str          # "gcn" | "mean" | "root"
     rel: int           # relation index (ignored for root)
     weight: torch.Tensor  # [f_out, f_in]
+    dst_type: int = -1    # multi-node-type: destination node type of the relation
 
 
 @dataclass
 class ConvLayer:
     terms: List[Term]
-    bias: torch.Tensor    # [f_out] (sum over relations)
+    bias: torch.Tensor    # [f_out] (sum over relations); multi-node-type: [n_types, f_out]
     act: Optional[str]
     f_in: int
     f_out: int
@@ -52,6 +60,8 @@ class ModelProgram:
     convs: List[ConvLayer] = field(default_factory=list)
     head: List[HeadLayer] = field(default_factory=list)
     out_col: int = 0
+    n_types: int = 1               # > 1: multi-node-type program (node-type-gated terms)
+    out_type: Optional[int] = None  # multi-node-type: node type whose rows feed the head
 
     @property
     def hops(self):
@@ -159,17 +169,81 @@ def _conv_layer(conv, rel_index):
     return terms, bias, f_in, f_out
 
 
-def compile_arch(arch: nn.Module, edge_type_names=None) -> ModelProgram:
+def _pad_cols(w, n):
+    return w if w.shape[1] == n else torch.nn.functional.pad(w, (0, n - w.shape[1]))
+
+
+def _conv_layer_multi(conv, rel_index, node_type_names):
+    """HeteroConv over several node types: terms gated by destination type, SAGE root weights
+    and biases summed per destination type.  Returns (terms, bias [n_types, f_out], f_in, f_out,
+    destination type of the first present relation)."""
+    if type(conv).__name__ != "HeteroConv" or getattr(conv, "aggr", "sum") != "sum":
+        raise UnsupportedArch("multi-node-type graphs need HeteroConv(aggr='sum') layers")
+    nt = len(node_type_names)
+    terms, roots, biases = [], {}, {}
+    f_out, first_dst, f_ins = None, None, []
+    for key, sub in conv.convs.items():
+        et = tuple(key.split("__"))
+        if et not in rel_index:
+            continue
+        s_t, d_t = node_type_names.index(et[0]), node_type_names.index(et[-1])
+        if type(sub).__name__ == "GCNConv" and s_t != d_t:
+            raise UnsupportedArch("GCNConv on a bipartite relation")
+        t, b, wr, fi, fo = _single_conv_terms(sub, rel_index[et])
+        if f_out is not None and fo != f_out:
+            raise UnsupportedArch("HeteroConv relations with different output widths")
+        f_out = fo
+        first_dst = d_t if first_dst is None else first_dst
+        for term in t:
+            term.dst_type = d_t
+            f_ins.append(term.weight.shape[1])
+        terms += t
+        if b is not None:
+            biases[d_t] = b.clone() if d_t not in biases else biases[d_t] + b
+        if wr is not None:
+            f_ins.append(wr.shape[1])
+            if d_t in roots and roots[d_t].shape != wr.shape:
+                raise UnsupportedArch("root weights of one destination type differ in shape")
+            roots[d_t] = wr.clone() if d_t not in roots else roots[d_t] + wr
+    if not terms:
+        raise UnsupportedArch("HeteroConv with no relation present in the graph")
+    # HeteroConv's output dict is keyed in edge_index_dict order (the graph's relation order)
+    for et in rel_index:
+        if "__".join(et) in conv.convs:
+            first_dst = node_type_names.index(et[-1])
+            break
+    for d_t in sorted(roots):
+        terms.append(Term("root", -1, roots[d_t], d_t))
+    f_in = max(f_ins)
+    for term in terms:
+        term.weight = _pad_cols(term.weight, f_in)
+    bias = torch.zeros(nt, f_out)
+    for d_t, b in biases.items():
+        bias[d_t] = b
+    return terms, bias, f_in, f_out, first_dst
+
+
+def compile_arch(arch: nn.Module, edge_type_names=None, node_type_names=None) -> ModelProgram:
     """Lower `arch` to a ModelProgram.  `edge_type_names` (list of (src, rel, dst) tuples in
-    homogenised edge-type order, data.py:743-822) enables HeteroConv relations."""
+    homogenised edge-type order, data.py:743-822) enables HeteroConv relations;
+    `node_type_names` with two or more types selects the multi-node-type lowering."""
     rel_index = None
     if edge_type_names is not None:
         rel_index = {tuple(et): i for i, et in enumerate(edge_type_names)}
+    multi = node_type_names is not None and len(node_type_names) >= 2
+    if multi and rel_index is None:
+        raise UnsupportedArch("multi-node-type graphs need edge types")
     units = list(_leaf_units(arch))
     prog = ModelProgram()
+    if multi:
+        prog.n_types = len(node_type_names)
     i = 0
     while i < len(units) and _is_conv(units[i]):
-        terms, bias, f_in, f_out = _conv_layer(units[i], rel_index)
+        if multi:
+            terms, bias, f_in, f_out, prog.out_type = _conv_layer_multi(units[i], rel_index,
+                                                                        list(node_type_names))
+        else:
+            terms, bias, f_in, f_out = _conv_layer(units[i], rel_index)
         act = None
         if i + 1 < len(units) and _act_name(units[i + 1]) is not None:
             act = _act_name(units[i + 1])

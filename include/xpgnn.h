@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 6
+#define XPG_ABI_VERSION 7
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -97,6 +97,8 @@ typedef struct xpg_term_desc {
   int32_t kind;            /* enum xpg_term                                             */
   int32_t rel;             /* relation index (degree slot); ignored for ROOT           */
   const float* table;      /* layer 1 only: pre-transformed F_0 rows [n0][f_out_pad]   */
+  int32_t dst_type;        /* multi-node-type plans: the term only reaches targets of   */
+                           /* this node type (HeteroConv relation destination); -1 = all */
 } xpg_term_desc;
 
 typedef struct xpg_layer_desc {
@@ -115,7 +117,10 @@ typedef struct xpg_layer_desc {
   const int32_t* self_mult;/* [n_rel * n_tgt] multiplicity of (t, t) edges             */
   xpg_term_desc terms[XPG_MAX_TERMS];
   const float* weight;     /* layer >= 2: [f_out_pad][n_terms * f_in_pad]               */
-  const float* bias;       /* [f_out_pad], summed over relations, zero-padded          */
+  const float* bias;       /* [n_types][f_out_pad], summed over relations, zero-padded */
+  const int32_t* tgt_type; /* multi-node-type plans: [n_tgt] node type of each target;   */
+                           /* NULL for homogeneous / single-node-type graphs             */
+  int32_t n_types;         /* rows of bias (1 when tgt_type is NULL)                   */
 } xpg_layer_desc;
 
 typedef struct xpg_head_desc {

@@ -94,6 +94,35 @@ class ConvStack(nn.Module):
         return x
 
 
+class HeteroSage(nn.Module):
+    """Multi-node-type [HeteroConv(SAGEConv) -> ReLU]* + Linear head on the first output node
+    type (the reference's multi-type arch layout, tests/test_utils.py:164-182, with SAGEConv in
+    place of GATConv — the shim restates SAGE; bipartite relations take (F_src, F_dst) inputs)."""
+
+    def __init__(self, rels, in_dims, hidden, n_layers, fc_dims):
+        super().__init__()
+        convs = []
+        for li in range(n_layers):
+            convs.append(HeteroConv({r: SAGEConv((in_dims[r[0]], in_dims[r[-1]]) if li == 0
+                                                 else (hidden, hidden), hidden) for r in rels},
+                                    aggr="sum"))
+            convs.append(nn.ReLU())
+        self.conv = nn.ModuleList(convs)
+        fcs = []
+        for i in range(len(fc_dims) - 1):
+            fcs.append(Linear(fc_dims[i], fc_dims[i + 1]))
+            fcs.append(nn.Sigmoid() if i == len(fc_dims) - 2 else nn.ReLU())
+        self.fc = nn.ModuleList(fcs)
+
+    def forward(self, x, edge_index):
+        for i, c in enumerate(self.conv):
+            x = c(x, edge_index) if i % 2 == 0 else {k: c(v) for k, v in x.items()}
+        x = x[list(x.keys())[0]]
+        for l in self.fc:
+            x = l(x)
+        return x
+
+
 def load_ckpt(name):
     sd = torch.load(os.path.join(REF_DATA, name), weights_only=True, map_location="cpu")["model"]
     return {k: v.clone() for k, v in sd.items()}
@@ -251,6 +280,34 @@ def case_hetero_single():
                         "hetero_rels": [list(r) for r in rels]})
 
 
+HM_RELS = [("A", "ab", "B"), ("B", "ba", "A"), ("A", "aa", "A"), ("C", "ca", "A"),
+           ("A", "ac", "C")]
+HM_SIZES = {"A": 50, "B": 30, "C": 20}
+HM_DIMS = {"A": 8, "B": 6, "C": 5}
+
+
+def case_hetero_multi():
+    """Three node types with different feature widths (padded by hetero2homo), five relations
+    (three bipartite), 2-layer HeteroConv(SAGEConv) — the multi-node-type path
+    (model.py:118-253, including quirk Q4: the per-copy outputs re-cut by
+    extract_node_edge_output)."""
+    g = torch.Generator().manual_seed(41)
+    feat = {t: torch.randn((n, HM_DIMS[t]), generator=g) for t, n in HM_SIZES.items()}
+    ei = {r: torch.stack([torch.randint(0, HM_SIZES[r[0]], (m,), generator=g),
+                          torch.randint(0, HM_SIZES[r[-1]], (m,), generator=g)])
+          for r, m in zip(HM_RELS, (60, 50, 70, 30, 30))}
+    torch.manual_seed(12)
+    arch = HeteroSage(HM_RELS, HM_DIMS, 16, 2, [16, 8, 1])
+    arch.eval()
+    names = {t: [f"{t.lower()}{i}" for i in range(n)] for t, n in HM_SIZES.items()}
+    torch.manual_seed(5)
+    run_case("hetero_multi", feat, ei, arch, dict(PARAMS, interpret_samples=16, epochs=4),
+             names, None, None, element_type="B", problem="node", element="b2", times=2,
+             arch_spec={"kind": "hetero_sage", "rels": [list(r) for r in HM_RELS],
+                        "sizes": HM_SIZES, "in_dims": HM_DIMS, "hidden": 16, "layers": 2,
+                        "fc": [16, 8, 1]})
+
+
 def case_sage_shapley():
     g = torch.Generator().manual_seed(5)
     n, e = 300, 1500
@@ -349,6 +406,10 @@ def extract_test_run_edges():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # regenerate selected cases only: make_golden.py hetero_multi ...
+        for c in sys.argv[1:]:
+            globals()["case_" + c]()
+        sys.exit(0)
     extract_test_run_edges()
     case_kernels()
     case_test_run(3, "test_run")
@@ -358,3 +419,4 @@ if __name__ == "__main__":
     case_sage_shapley()
     case_gcn2_graph()
     case_gcn2_medium()
+    case_hetero_multi()

@@ -76,3 +76,51 @@ def _conv_params(kind, sd, p):
         return {"W": sd[p + "lin.weight"], "b": sd.get(p + "bias")}
     return {"Wl": sd[p + "lin_l.weight"], "bl": sd.get(p + "lin_l.bias"),
             "Wr": sd[p + "lin_r.weight"]}
+
+
+def hetero_multi_setup(z, meta):
+    """The multi-node-type golden case as the reference sees it after Explainer's host steps
+    (see multi_type_setup)."""
+    feat, ei = case_inputs(z)
+    a = meta["arch_spec"]
+    return multi_type_setup(feat, ei, meta["names"], meta["element"], meta["element_type"],
+                            a["layers"], state_dict(z), a["fc"])
+
+
+def multi_type_setup(feat, ei, names_by_type, element, element_type, n_layers, sd, fc_dims):
+    """hetero2homo (type blocks in feat-dict order, features zero-padded to the widest type,
+    relation edges shifted by the node-type pointers, data.py:95-147,695-822), the L+1-hop
+    computational subgraph of the element, and sub_ind = the element's position among the
+    subgraph nodes of its type (explainer.py:449-463); oracle spec of a HeteroSageStack state
+    dict.  Returns a dict."""
+    import oracle
+    ntypes = list(feat.keys())
+    rels = list(ei.keys())
+    wmax = max(v.shape[1] for v in feat.values())
+    pads = [wmax - feat[t].shape[1] for t in ntypes]
+    ptr = np.cumsum([0] + [feat[t].shape[0] for t in ntypes])[:-1]
+    x = np.vstack([np.pad(feat[t], ((0, 0), (0, wmax - feat[t].shape[1]))) for t in ntypes])
+    nt = np.concatenate([np.full(feat[t].shape[0], i) for i, t in enumerate(ntypes)])
+    e = np.hstack([ei[r] + np.array([[ptr[ntypes.index(r[0])]], [ptr[ntypes.index(r[-1])]]])
+                   for r in rels])
+    et = np.concatenate([np.full(ei[r].shape[1], i) for i, r in enumerate(rels)])
+    names = [n for t in ntypes for n in names_by_type[t]]
+    q = names.index(element)
+    subset, sub_ei, _, emask = oracle.comp_graph(q, n_layers, e, x.shape[0])
+    sub_nt, sub_et = nt[subset], et[emask]
+    sub_names = [names[i] for i in subset]
+    etype = ntypes.index(element_type)
+    filt = [n for n, t in zip(sub_names, sub_nt) if t == etype]
+    layers = []
+    for li in range(n_layers):
+        layers.append({r: {"Wl": sd[f"conv.{2 * li}.convs.{'__'.join(r)}.lin_l.weight"],
+                           "bl": sd.get(f"conv.{2 * li}.convs.{'__'.join(r)}.lin_l.bias"),
+                           "Wr": sd[f"conv.{2 * li}.convs.{'__'.join(r)}.lin_r.weight"]}
+                       for r in rels})
+    nfc = len(fc_dims) - 1
+    fc = [{"W": sd[f"fc.{2 * i}.weight"], "b": sd[f"fc.{2 * i}.bias"],
+           "act": "sigmoid" if i == nfc - 1 else "relu"} for i in range(nfc)]
+    return {"x": x[subset], "nt": sub_nt, "ei": sub_ei, "et": sub_et, "ntypes": ntypes,
+            "rels": rels, "pads": pads, "sub_ind": filt.index(element),
+            "spec": {"layers": layers, "fc": fc}, "sub_names": sub_names, "feat": feat,
+            "edge_index": ei}

@@ -530,3 +530,92 @@ def test_comp_graph_device_matches_host():
         b = Data(feat.to(DEV), ei.to(DEV)).comp_graph(q, 2, "node_prediction", names)
         assert torch.equal(a[0], b[0].cpu()) and torch.equal(a[1], b[1].cpu())
         assert a[2] == b[2] and int(a[3]) == int(b[3])
+
+
+# ------------------------------------------------------------------ multi-node-type hetero (§8a6/f2)
+def _mt_plan(c, arch):
+    from bikg_graph_explainability_public_amd import pipeline
+    x = torch.as_tensor(c["x"], dtype=torch.float32, device=DEV)
+    ei = torch.as_tensor(c["ei"], device=DEV)
+    nt = torch.as_tensor(c["nt"], device=DEV)
+    et = torch.as_tensor(c["et"], device=DEV)
+    plan = pipeline.build_plan(arch, x, ei, [c["sub_ind"]], nt, et, c["ntypes"], c["rels"],
+                               c["pads"])
+    return plan, ei
+
+
+def _mt_check(c, arch, masks, atol=1e-5):
+    from bikg_graph_explainability_public_amd import pipeline
+    e = _eng()
+    plan, ei = _mt_plan(c, arch)
+    assert plan is not None and plan.multi_type
+    S = c["x"].shape[0]
+    for m in masks:
+        bits = e.pack_masks(torch.as_tensor(m, device=DEV))
+        y = plan.forward(bits)[:, 0]
+        y = torch.where(pipeline.empty_copy_rows(bits, S, ei), torch.zeros_like(y), y)
+        ref = oracle.hetero_multi_copy_outputs(c["spec"], c["x"], c["nt"], c["ei"], c["et"],
+                                               c["ntypes"], c["rels"], c["pads"], m,
+                                               c["sub_ind"])
+        np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=0, atol=atol)
+
+
+def test_multi_type_engine_vs_oracle_golden():
+    """Node-type-gated HIP forward (unfused path) vs the oracle's per-copy restatement of
+    Model.predict_hetero_output on the reference-recorded masks of tests/golden/hetero_multi."""
+    from case_builders import build_arch
+    from golden_utils import hetero_multi_setup
+    z, meta = load_case("hetero_multi")
+    c = hetero_multi_setup(z, meta)
+    _mt_check(c, build_arch(meta, z).to(DEV), repeat_masks(z, meta))
+
+
+@pytest.mark.parametrize("hidden,layers", [(64, 2), (32, 3), (128, 1)])
+def test_multi_type_engine_vs_oracle_random(hidden, layers):
+    """Three node types of different widths, five relations (three bipartite), all-off /
+    all-on / sparse rows."""
+    from bikg_graph_explainability_public_amd.nn import HeteroSageStack
+    from golden_utils import multi_type_setup
+    rels = [("A", "ab", "B"), ("B", "ba", "A"), ("A", "aa", "A"), ("C", "ca", "A"),
+            ("A", "ac", "C")]
+    sizes, dims = {"A": 300, "B": 200, "C": 150}, {"A": 24, "B": 16, "C": 40}
+    g = torch.Generator().manual_seed(hidden + layers)
+    feat = {t: torch.randn(n, dims[t], generator=g).numpy() for t, n in sizes.items()}
+    ei = {r: torch.stack([torch.randint(0, sizes[r[0]], (m,), generator=g),
+                          torch.randint(0, sizes[r[-1]], (m,), generator=g)]).numpy()
+          for r, m in zip(rels, (900, 700, 800, 400, 400))}
+    torch.manual_seed(3)
+    arch = HeteroSageStack(rels, dims, hidden, layers, [hidden, 16, 1]).eval()
+    names = {t: [f"{t.lower()}{i}" for i in range(n)] for t, n in sizes.items()}
+    c = multi_type_setup(feat, ei, names, "b7", "B", layers,
+                         {k: v.numpy() for k, v in arch.state_dict().items()}, [hidden, 16, 1])
+    S = c["x"].shape[0]
+    gm = np.random.default_rng(layers)
+    m = gm.random((96, S)) < 0.5
+    m[0] = False
+    m[1] = True
+    m[2] = gm.random(S) < 0.05
+    _mt_check(c, arch.to(DEV), [m])
+
+
+@pytest.mark.parametrize("path", ["engine", "generic"])
+def test_multi_type_explainer_run_matches_reference(path, monkeypatch):
+    """Explainer.run on the multi-node-type golden case (quirk Q4 reproduced) vs the
+    reference's DataFrames: the HIP engine and the batched generic path."""
+    from bikg_graph_explainability_public_amd import pipeline
+    from case_builders import build_explainer
+    if path == "generic":
+        monkeypatch.setattr(pipeline, "build_plan", lambda *a, **k: None)
+    exp, z, meta = build_explainer("hetero_multi")
+    torch.set_rng_state(torch.as_tensor(z["rng_state"]))
+    df, _ = exp.run(meta["element"], meta["times"])
+    assert exp.last_run["engine"] == (path == "engine")
+    for i in range(meta["times"]):
+        np.testing.assert_allclose(exp.last_run["repeats"][i]["y"].cpu().numpy().reshape(-1, meta[
+            f"r{i}_batch_size"])[:, 0], z[f"r{i}_output"], rtol=0, atol=1e-5)
+    ref = meta["df"]
+    got = df.reindex(ref["index"])
+    np.testing.assert_allclose(got["config_value_mean"].values, ref["config_value_mean"],
+                               atol=1e-4, rtol=0)
+    np.testing.assert_allclose(got["config_value_std"].values, ref["config_value_std"],
+                               atol=1e-4, rtol=0)
