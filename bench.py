@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=12800)
     p.add_argument("--full-graph-rows", type=int, default=64,
                    help="regime (ii): mask rows of the c3-shaped full-graph forward (0 = skip)")
+    p.add_argument("--no-hetero", action="store_true", help="skip the c4 multi-type section")
     p.add_argument("--no-graph-prediction", action="store_true",
                    help="skip the c3 graph_prediction per-query pipeline section")
     return p.parse_args()
@@ -347,6 +348,101 @@ def graph_prediction_section(args, dev):
             "sampler_GBps": R * W * 4 / (ph["sample"] * 1e-3) / 1e9}
 
 
+C4_RELS = [("gene", "interacts", "gene"), ("gene", "encodes", "protein"),
+           ("protein", "binds", "protein"), ("drug", "targets", "protein"),
+           ("protein", "regulates", "gene")]
+
+
+def hetero_c4_section(args, dev):
+    """c4 (BASELINE.json configs[3]): 3 node types (200k gene / 200k protein / 100k drug,
+    84 / 64 / 32 features), 5 relations (3 bipartite), 5M edges, one HeteroConv(SAGE) layer
+    (gcn_hetero_1hop shape: 84 -> 16, head 16 -> 16 -> 32 -> 1; GCNConv cannot take bipartite
+    relations), node_prediction of gene 7 through Explainer's host steps (hetero2homo, k-hop
+    subgraph on the GPU), then per repeat: device Shapley masks -> node-type-gated forward ->
+    empty-copy / Q4 targets -> KernelSHAP -> surrogate fit.  Regime (i): the subgraph is
+    cache-resident, so samples/s is the figure (no HBM fraction).  `reference_loop` times the
+    reference's own per-copy multi-type loop (model.py:196-249, one arch call + host sync per
+    row) on the same GPU for one batch."""
+    from bikg_graph_explainability_public_amd import engine, pipeline
+    from bikg_graph_explainability_public_amd.data import Data
+    from bikg_graph_explainability_public_amd.model import Model
+    from bikg_graph_explainability_public_amd.nn import HeteroSageStack
+    sizes = {"gene": 200_000, "protein": 200_000, "drug": 100_000}
+    dims = {"gene": 84, "protein": 64, "drug": 32}
+    g = torch.Generator(device=dev).manual_seed(4)
+    feat = {t: torch.randn((n, dims[t]), generator=g, device=dev) for t, n in sizes.items()}
+    ei = {r: torch.stack([torch.randint(0, sizes[r[0]], (1_000_000,), generator=g, device=dev),
+                          torch.randint(0, sizes[r[-1]], (1_000_000,), generator=g, device=dev)])
+          for r in C4_RELS}
+    torch.manual_seed(0)
+    arch = HeteroSageStack(C4_RELS, dims, 16, 1, [16, 16, 32, 1]).to(dev).eval()
+    d = Data(feat, ei)
+    fh, eh, nt, et, _, _, pads = d.hetero2homo()
+    ntn, etn = list(feat), list(ei)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sub_x, sub_ei, _, sub_ind, sub_nt, sub_et = Data(fh, eh).comp_graph(
+        7, 1, "node", [str(i) for i in range(fh.shape[0])], nt, et)
+    torch.cuda.synchronize()
+    t_khop = time.perf_counter() - t0
+    sub_nt = sub_nt.long()
+    q = int(sub_ind)  # gene = type 0 comes first in the sorted subset: position among genes
+    plan = pipeline.build_plan(arch, sub_x, sub_ei, [q], sub_nt, sub_et, ntn, etn, pads)
+    assert plan is not None and plan.multi_type
+    S = sub_x.shape[0]
+    R, epochs = 256 * 50, 50
+    batch = R // epochs
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    w0 = torch.zeros(S, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def rep(i, ev=None):
+        if ev:
+            ev[0].record(stream)
+        bits, cnt = engine.sample_shapley(900 + i, R, S, dev, with_counts=True)
+        if ev:
+            ev[1].record(stream)
+        y = plan.forward(bits)[:, 0]
+        empty = pipeline.empty_copy_rows(bits, S, sub_ei)
+        y = pipeline.multi_type_targets(y, empty, batch, q, S, q4=False)
+        if ev:
+            ev[2].record(stream)
+        k = engine.shap_kernel(bits, S, counts=cnt)
+        if ev:
+            ev[3].record(stream)
+        engine.wlm_fit(bits, S, batch, y, k, w0, params)
+        if ev:
+            ev[4].record(stream)
+
+    rep(0)
+    torch.cuda.synchronize()
+    reps = 5
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(reps)]
+    t0 = time.perf_counter()
+    for i in range(reps):
+        rep(1 + i, evs[i])
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    ph = {name: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in evs]))
+          for j, name in enumerate(("sample", "forward", "shap", "wlm"))}
+    # the reference's per-copy loop on the same GPU, one batch of rows
+    mask = engine.unpack_masks(engine.sample_shapley(77, batch, S, dev), S)
+    cf, cnt_t, pei, pet = Data(sub_x, sub_ei).perturbator(mask, "node", sub_nt, sub_et)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    Model(arch).predict_hetero_output(cf, pei.long(), cnt_t, pet, ntn, etn, batch, S, q, pads, "node")
+    torch.cuda.synchronize()
+    loop_rate = batch / (time.perf_counter() - t0)
+    return {"workload": "c4: 3 node types (200k/200k/100k, 84/64/32 feats), 5 relations (3 "
+                        "bipartite), 5M edges, HeteroConv(SAGE) 1 layer 84->16 + head "
+                        "16->16->32->1, node_prediction of gene 7, interpret_samples=256 x "
+                        "epochs=50 = 12,800 rows, one repeat, per-copy targets (hetero_q4=False)",
+            "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
+            "khop_ms": t_khop * 1e3, "ms_per_repeat": wall * 1e3,
+            "samples_per_s": R / wall, "phases_ms": ph,
+            "reference_loop_gpu_samples_per_s": loop_rate}
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -470,6 +566,9 @@ def main():
                 torch.cuda.empty_cache()
             if args.full_graph_rows > 0:
                 regimes["full_graph_c3"] = full_graph_section(args, dev)
+                torch.cuda.empty_cache()
+            if not args.no_hetero:
+                regimes["hetero_c4"] = hetero_c4_section(args, dev)
                 torch.cuda.empty_cache()
             if regimes:
                 line["regimes"] = regimes
