@@ -1582,7 +1582,7 @@ __global__ __launch_bounds__(512) void k_wide_l1m(const WideArgs a) {
 //     registers, K = 8 KW; else read from L2), bias + act, the dense head on the tile, and the
 //     output column for the 32 samples.
 template <int NFI, bool LAST, int KW>
-__global__ __launch_bounds__(256, LAST ? 2 : (NFI >= 12 ? 2 : 3)) void k_wide_tgt(const WideArgs a) {
+__global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >= 12 ? 2 : 3)) void k_wide_tgt(const WideArgs a) {
   constexpr int RIF = (LAST && KW > 0) || NFI >= 8 ? 4 : 8;  // rows in flight per 16-lane group
   extern __shared__ __attribute__((aligned(16))) float wsm[];
   float* A = wsm;  // LAST: [32][a_ld]
@@ -1791,38 +1791,49 @@ __global__ __launch_bounds__(256, LAST ? 2 : (NFI >= 12 ? 2 : 3)) void k_wide_tg
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wreg[kk].z, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wreg[kk].w, acc, 0, 0, 0);
         }
-      } else {  // weights streamed from L2, PF float4 loads ahead; two independent MFMA chains
-        constexpr int PF = 8;
+      } else {
+        // weights streamed from L2 through a ring of 4 float4 per lane: each slot is refilled
+        // right after its MFMAs with an unconditional (clamped) load, so no loop-carried copy
+        // forces a wait — the load lands one iteration (16 MFMAs) later.  The A tile (LDS) is
+        // read half an iteration ahead.  Two independent accumulation chains; K % 32 == 0.
         const float* wp = a.weight + (int64_t)(nb * 32 + i32) * a.K + 4 * h;
-        float4 wb[PF];
-#pragma unroll
-        for (int j = 0; j < PF; ++j)
-          wb[j] = j * 8 < a.K ? *reinterpret_cast<const float4*>(wp + j * 8) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int klast = a.K - 8;
+        auto ldw = [&](int k) { return *reinterpret_cast<const float4*>(wp + (k < klast ? k : klast)); };
+        auto lda = [&](int k) { return *reinterpret_cast<const float4*>(ap + k); };
+        float4 w0 = ldw(0), w1 = ldw(8), w2 = ldw(16), w3 = ldw(24);
+        float4 a0 = lda(0), a1 = lda(8);
+        __builtin_amdgcn_sched_barrier(0);
         f32x16 acc2;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc2[q] = 0.f;
-        for (int kc0 = 0; kc0 < a.K; kc0 += 8 * PF) {  // K % 16 == 0 (host check)
-#pragma unroll
-          for (int j = 0; j < PF; j += 2) {
-            const int kc = kc0 + 8 * j;
-            if (kc < a.K) {
-              const float4 av = *reinterpret_cast<const float4*>(ap + kc);
-              const float4 av2 = *reinterpret_cast<const float4*>(ap + kc + 8);
-              const float4 wv = wb[j], wv2 = wb[j + 1];
-              if (kc + 8 * PF < a.K) {
-                wb[j] = *reinterpret_cast<const float4*>(wp + kc + 8 * PF);
-                wb[j + 1] = *reinterpret_cast<const float4*>(wp + kc + 8 + 8 * PF);
-              }
-              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wv.x, acc, 0, 0, 0);
-              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.x, wv2.x, acc2, 0, 0, 0);
-              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wv.y, acc, 0, 0, 0);
-              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.y, wv2.y, acc2, 0, 0, 0);
-              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wv.z, acc, 0, 0, 0);
-              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.z, wv2.z, acc2, 0, 0, 0);
-              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wv.w, acc, 0, 0, 0);
-              acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2.w, wv2.w, acc2, 0, 0, 0);
-            }
-          }
+        for (int kc = 0; kc < a.K; kc += 32) {
+          const float4 a2 = lda(kc + 16), a3 = lda(kc + 24);
+          __builtin_amdgcn_sched_barrier(0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, w0.x, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, w1.x, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, w0.y, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, w1.y, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, w0.z, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, w1.z, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, w0.w, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, w1.w, acc2, 0, 0, 0);
+          w0 = ldw(kc + 32);
+          w1 = ldw(kc + 40);
+          const int kn = kc + 32 < a.K ? kc + 32 : 0;
+          a0 = lda(kn);
+          a1 = lda(kn + 8);
+          __builtin_amdgcn_sched_barrier(0);  // keep the refills here (the scheduler sinks them to the use)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.x, w2.x, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.x, w3.x, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.y, w2.y, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.y, w3.y, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.z, w2.z, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.z, w3.z, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.w, w2.w, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.w, w3.w, acc2, 0, 0, 0);
+          w2 = ldw(kc + 48);
+          w3 = ldw(kc + 56);
+          __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
@@ -3125,7 +3136,7 @@ int wide_layout(const xpg_forward_plan* p, WideWs* W) {
   if (f1 % 16) return 1;
   if (W->nfi != 2 && W->nfi != 4 && W->nfi != 8 && W->nfi != 12 && W->nfi != 16) return 1;
   const int K = l2.n_terms * l2.f_in_pad;
-  if (K % 16 || l2.f_out_pad % 32 || l2.f_out_pad > 256) return 1;
+  if (K % 32 || l2.f_out_pad % 32 || l2.f_out_pad > 256) return 1;
   int hw = l2.f_out_pad, cur = l2.f_out_pad;
   for (int i = 0; i < p->n_head; ++i) {
     if (p->head[i].k_pad != cur || p->head[i].n_pad > 256) return 1;
@@ -3140,8 +3151,11 @@ int wide_layout(const xpg_forward_plan* p, WideWs* W) {
   W->a_ld = K + 4;
   W->h_ld = hw + 4;
   W->o_h0 = 32 * W->a_ld;
-  int off_f = W->o_h0 + 32 * W->h_ld;
-  if (W->h_ld <= W->a_ld) {
+  // a single-logit head is fused into the MFMA epilogue: H0 then holds one partial per
+  // (column block, sample) only — the smaller LDS footprint lets more workgroups share a CU
+  const bool head1 = p->n_head == 1 && p->head[0].n_real == 1 && p->out_col == 0;
+  int off_f = W->o_h0 + (head1 ? ((l2.f_out_pad + 3) & ~3) : 32 * W->h_ld);
+  if (head1 || W->h_ld <= W->a_ld) {
     W->o_h1 = 0;  // the second head tile reuses the A tile (dead after the MFMA)
   } else {
     W->o_h1 = off_f;

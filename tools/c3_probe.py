@@ -42,6 +42,7 @@ def main():
     p.add_argument("--rows-b", type=int, default=4)
     p.add_argument("--skip-a", action="store_true")
     p.add_argument("--skip-b", action="store_true")
+    p.add_argument("--dbg", default="0,1,2,3,4,8,12", help="XPG_WIDE_DBG values to time in B")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     _lib.load()
@@ -91,7 +92,7 @@ def main():
         print(f"[B] plan (all targets): n0={plan.n0} in {time.time() - t0:.1f}s", flush=True)
         rb = args.rows_b
         bits = engine.sample_shapley(13, rb, N, dev)
-        for dbg in ("0", "1", "2", "3", "4", "8", "12"):
+        for dbg in args.dbg.split(","):
             os.environ["XPG_WIDE_DBG"] = dbg
             ms, y = timed(lambda: plan.forward(bits), reps=2)
             print(f"[B] full forward (XPG_WIDE_DBG={dbg}) {rb} rows x {N} targets: {ms:.3f} ms = "
