@@ -47,6 +47,17 @@ inline int words_of(int64_t cols) { return static_cast<int>((cols + 31) / 32); }
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup fence on every address
+// space: it waits for vmcnt(0), i.e. for every global load still in flight (prefetches of the
+// next item) and every global store.  Where a workgroup shares data only through LDS the fence is
+// narrowed to LDS ("local"), so the barrier waits for lgkmcnt(0) alone and register prefetches
+// stay in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ bool bit_of(const uint32_t* row, int c) {
   return (row[c >> 5] >> (c & 31)) & 1u;
 }
@@ -1415,10 +1426,6 @@ constexpr int kL1Cap = 128;  // entries per target staged in LDS per round (more
 // loads and stores in order: a wave that stored target t would wait for those stores before
 // using its loads of target t + 1.  Barriers are plain s_barrier (LDS drained by lgkmcnt), never
 // a fence on global memory, so the store waves never wait for their stores either.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
 
 __global__ __launch_bounds__(512) void k_wide_l1m(const WideArgs a) {
   extern __shared__ __attribute__((aligned(16))) float ctile[];  // [32][w_row + 4]
@@ -1653,7 +1660,7 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
   }
   for (int t = blockIdx.x; t < a.n_tgt; t += gridDim.x) {
     const int tn = t + gridDim.x;
-    __syncthreads();  // the previous item's readers of E / A / the head tiles are done
+    lds_barrier();  // the previous item's readers of E / A / the head tiles are done
     const int total = pf_seg[XPG_MAX_TERMS];
     const bool staged = total <= kWideCap;
     if (staged && tid < total) {
@@ -1668,7 +1675,7 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
     const int tf0 = pf_tf0, tp = pf_tp;
     const uint32_t mv = pf_mv;
     if (tn < a.n_tgt) prefetch_idx(tn);
-    __syncthreads();
+    lds_barrier();
     // ---- gather: group g owns samples s0 = g and s1 = g + 16
     {
       const int s0 = g, s1 = g + 16;
@@ -1774,7 +1781,7 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
     }
     if (tn < a.n_tgt) prefetch_m();
     if (!LAST || (a.dbg & 1)) continue;
-    __syncthreads();
+    lds_barrier();
     // ---- dense: C[32 samples x f_out_pad] = act(A W^T + b), wave = 32-column blocks
     float* H0 = wsm + a.o_h0;
     for (int nb = wave; nb * 32 < a.f_out_pad && !(a.dbg & 8); nb += 4) {
@@ -1862,7 +1869,7 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (a.head1) {  // y[s] = act(sum over column blocks + b)
       if (tid < a.nr) {
         float v = 0.f;
@@ -1896,7 +1903,7 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
         }
         nxt[ss * a.h_ld + n] = v;
       }
-      __syncthreads();
+      lds_barrier();
       float* tmp = cur;
       cur = nxt;
       nxt = tmp;
@@ -2049,6 +2056,13 @@ __device__ __forceinline__ float nib8(const float* tab, uint32_t word) {
 // STAGE: the step's mask rows ([batch][rp]), column bit vectors ([cols][cp]) and kernel weights
 // live in LDS; the next copies are loaded into registers right after a barrier and written to
 // LDS just before a later one, so their global latency hides behind a phase.
+// Unstaged fits keep the w tables in global memory (t_glob), so their barriers fence it too.
+template <bool STAGE>
+__device__ __forceinline__ void wlm_barrier() {
+  if (STAGE) lds_barrier();
+  else __syncthreads();
+}
+
 template <int CPT, bool STAGE>
 __global__ __launch_bounds__(1024) void k_wlm_fit(
     const uint32_t* __restrict__ bits, const uint32_t* __restrict__ colbits, int64_t rows,
@@ -2102,7 +2116,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
   for (int e = tid; e < ngrp_alloc * kTabPitch; e += 1024) G[e] = 0.f;
   wlm_build_T<CPT>(w, T, ntab);
 
-  uint32_t stg[kStage];
+  uint32_t stg[kStage] = {};  // loaded only where a stage has data; the rest are stored, never read
   double kst = 0.0;
   // stage-load helpers (flat element index q*1024 + tid over the buffer's logical extent)
 #define XPG_ROWS_LOAD(TT)                                                               \
@@ -2110,14 +2124,12 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     const int64_t r0_ = (TT) * batch;                                                   \
     const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);      \
     const uint32_t* src_ = bits + r0_ * words;                                          \
+    const int n_ = B_ * words;                                                          \
     _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
       const int e_ = q * 1024 + tid;                                                    \
-      const int n_ = B_ * words;                                                        \
-      const uint32_t x_ = src_[e_ < n_ ? e_ : n_ - 1];                                  \
-      stg[q] = e_ < n_ ? x_ : 0u;                                                       \
+      if (q * 1024 < n_) stg[q] = src_[e_ < n_ ? e_ : n_ - 1];                          \
     }                                                                                   \
-    const double k_ = kern[r0_ + (tid < B_ ? tid : B_ - 1)];                            \
-    kst = tid < B_ ? k_ : 0.0;                                                          \
+    kst = kern[r0_ + (tid < B_ ? tid : B_ - 1)];                                        \
   }
 #define XPG_ROWS_STORE(TT)                                                              \
   {                                                                                     \
@@ -2135,8 +2147,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     const uint32_t* src_ = colbits + (TT) * cols * bw;                                  \
     _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
       const int e_ = q * 1024 + tid;                                                    \
-      const uint32_t x_ = src_[e_ < cols * bw ? e_ : cols * bw - 1];                    \
-      stg[q] = e_ < cols * bw ? x_ : 0u;                                                \
+      if (q * 1024 < cols * bw) stg[q] = src_[e_ < cols * bw ? e_ : cols * bw - 1];     \
     }                                                                                   \
   }
 #define XPG_COLS_STORE()                                                                \
@@ -2153,7 +2164,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     XPG_ROWS_LOAD(0)
     XPG_ROWS_STORE(0)
   }
-  __syncthreads();
+  wlm_barrier<STAGE>();
 #ifdef XPG_WLM_STAMPS
   uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t stamp_last = __builtin_amdgcn_s_memtime();
@@ -2195,7 +2206,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       if (j < batch) bpart[sl * batch + j] = s;
     }
     XPG_STAMP(0)
-    __syncthreads();  // bpart complete
+    wlm_barrier<STAGE>();  // bpart complete
     XPG_STAMP(1)
     // ---- G: g_j = 2 k_j (p_j - ybar) / (B sum k) and the nibble tables of g over 4-row groups
     {
@@ -2222,7 +2233,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     }
     if (STAGE) XPG_COLS_STORE()
     XPG_STAMP(2)
-    __syncthreads();  // G and Cb(t) complete; Rb, kbuf free
+    wlm_barrier<STAGE>();  // G and Cb(t) complete; Rb, kbuf free
     XPG_STAMP(3)
     if (STAGE && t + 1 < nsteps) XPG_ROWS_LOAD(t + 1)
     // ---- D: partial gradient (M_b^T g)_i over a slice of the column's row words (lanes = columns)
@@ -2251,7 +2262,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
       dpart[sl * cpad + i] = s;
     }
     XPG_STAMP(4)
-    __syncthreads();  // dpart complete
+    wlm_barrier<STAGE>();  // dpart complete
     XPG_STAMP(5)
     // ---- L1 subgradient + L2 decay; Adam (torch single-tensor order) on the owned columns
 #pragma unroll
@@ -2272,7 +2283,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
     wlm_build_T<CPT>(w, T, ntab);
     if (STAGE && t + 1 < nsteps) XPG_ROWS_STORE(t + 1)
     XPG_STAMP(6)
-    __syncthreads();
+    wlm_barrier<STAGE>();
     XPG_STAMP(7)
   }
 #ifdef XPG_WLM_STAMPS
@@ -2378,7 +2389,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
   for (int e = tid; e < ngrp_alloc * kTabPitch; e += 1024) G[e] = 0.f;
   wlm_build_T<CPT>(w, T, ow * 8);
 
-  uint32_t stg[kStage];
+  uint32_t stg[kStage] = {};  // loaded only where a stage has data; the rest are stored, never read
   double kst = 0.0;
 #define XPG_MC_ROWS_LOAD(TT)                                                            \
   {                                                                                     \
@@ -2387,13 +2398,13 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     const int n_ = B_ * ow;                                                             \
     _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
       const int e_ = q * 1024 + tid;                                                    \
-      const int ee_ = e_ < n_ ? e_ : (n_ > 0 ? n_ - 1 : 0);                             \
-      const int rr_ = ow > 0 ? ee_ / ow : 0;                                            \
-      const uint32_t x_ = ow > 0 ? bits[(r0_ + rr_) * words + w_lo + (ee_ - rr_ * ow)] : 0u; \
-      stg[q] = e_ < n_ ? x_ : 0u;                                                       \
+      if (q * 1024 < n_) {                                                              \
+        const int ee_ = e_ < n_ ? e_ : n_ - 1;                                          \
+        const int rr_ = ee_ / ow;                                                       \
+        stg[q] = bits[(r0_ + rr_) * words + w_lo + (ee_ - rr_ * ow)];                   \
+      }                                                                                 \
     }                                                                                   \
-    const double k_ = kern[r0_ + (tid < B_ ? tid : B_ - 1)];                            \
-    kst = tid < B_ ? k_ : 0.0;                                                          \
+    kst = kern[r0_ + (tid < B_ ? tid : B_ - 1)];                                        \
   }
 #define XPG_MC_ROWS_STORE(TT)                                                           \
   {                                                                                     \
@@ -2412,8 +2423,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     const int n_ = ncol * bw;                                                           \
     _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
       const int e_ = q * 1024 + tid;                                                    \
-      const uint32_t x_ = n_ > 0 ? src_[e_ < n_ ? e_ : n_ - 1] : 0u;                    \
-      stg[q] = e_ < n_ ? x_ : 0u;                                                       \
+      if (q * 1024 < n_) stg[q] = src_[e_ < n_ ? e_ : n_ - 1];                          \
     }                                                                                   \
   }
 #define XPG_MC_COLS_STORE()                                                             \
@@ -2425,7 +2435,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
   }
   XPG_MC_ROWS_LOAD(0)
   XPG_MC_ROWS_STORE(0)
-  __syncthreads();
+  lds_barrier();
 #ifdef XPG_WLM_STAMPS
   uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t stamp_last = __builtin_amdgcn_s_memtime();
@@ -2467,7 +2477,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
       if (j < batch) bpart[sl * batch + j] = s;
     }
     XPG_STAMP(0)
-    __syncthreads();
+    lds_barrier();
     XPG_STAMP(1)
     // ---- exchange: publish this slice's partial p_j as 8-byte {value, step tag} granules
     // (write-through sc1 stores; parity double-buffered), then poll every slice's granule of
@@ -2498,7 +2508,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
       }
       xv[q * batch + j] = __uint_as_float(static_cast<uint32_t>(gr));
     }
-    __syncthreads();
+    lds_barrier();
     // ... p_j = their sum in slice order (identical in every workgroup), g_j
     {
       const double cg = 2.0 / (static_cast<double>(B) * sc.ksum);
@@ -2510,7 +2520,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
       }
     }
     XPG_STAMP(4)
-    __syncthreads();
+    lds_barrier();
     {
       const int ngrp = (B + 3) >> 2;
       for (int e = tid; e < ngrp * 16; e += 1024) {
@@ -2524,7 +2534,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
         G[grp * kTabPitch + vv] = acc;
       }
     }
-    __syncthreads();  // G and Cb(t) complete; Rb, kbuf free
+    lds_barrier();  // G and Cb(t) complete; Rb, kbuf free
     XPG_STAMP(5)
     if (t + 1 < nsteps) XPG_MC_ROWS_LOAD(t + 1)
     // ---- D: gradient of the own columns (lanes = columns)
@@ -2552,7 +2562,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
       }
       if (i < cpad) dpart[sl * cpad + i] = s;
     }
-    __syncthreads();
+    lds_barrier();
     XPG_STAMP(6)
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
@@ -2571,7 +2581,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     }
     wlm_build_T<CPT>(w, T, ow * 8);
     if (t + 1 < nsteps) XPG_MC_ROWS_STORE(t + 1)
-    __syncthreads();
+    lds_barrier();
     XPG_STAMP(7)
   }
 #ifdef XPG_WLM_STAMPS
