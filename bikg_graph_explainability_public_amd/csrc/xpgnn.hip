@@ -2366,8 +2366,8 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
   float* G = reinterpret_cast<float*>(smem);                         // [ngrp_alloc][17]
   float* bpart = G + ngrp_alloc * kTabPitch;                          // [n_bs][batch]
   float* dpart = bpart + n_bs * batch;                                // [n_ds][cpad]
-  float* pg = dpart + n_ds * cpad;                                    // [batch] g_j
-  float* xv = pg + batch;                                             // [P][batch] partials
+  // dpart is followed by [batch + P * batch] floats no longer used (the exchange is reduced in
+  // registers); kept so the layout matches wlm_layout's byte count
   const int kb_off = (ngrp_alloc * kTabPitch + n_bs * batch + n_ds * cpad + batch + P * batch + 1) & ~1;
   double* kbuf = reinterpret_cast<double*>(G + kb_off);              // [batch]
   float* T = reinterpret_cast<float*>(kbuf + batch);                 // [ow_max*8][17]
@@ -2492,48 +2492,55 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     XPG_MC_COLS_STORE()
     XPG_STAMP(2)
     XPG_STAMP(3)
-    // ---- gather the P partials of every row (thread per (slice, row) granule) ...
-    for (int e = tid; e < P * B; e += 1024) {
-      const int q = e / B, j = e - q * B;
-      const uint64_t* src = xs + q * (int64_t)batch + j;
-      uint64_t gr = ld64_sc1(src);
-      uint32_t n = 0;
-      while (static_cast<uint32_t>(gr >> 32) != tag) {
-        __builtin_amdgcn_s_sleep(1);
-        gr = ld64_sc1(src);
-        if (++n > kMcSpinLimit) {
-          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-      xv[q * batch + j] = __uint_as_float(static_cast<uint32_t>(gr));
-    }
-    lds_barrier();
-    // ... p_j = their sum in slice order (identical in every workgroup), g_j
-    {
-      const double cg = 2.0 / (static_cast<double>(B) * sc.ksum);
-      for (int j = tid; j < B; j += 1024) {
-        float p = 0.f;
-        for (int q = 0; q < P; ++q) p += xv[q * batch + j];
-        if (part == 0) p_hist[r0 + j] = p;
-        pg[j] = static_cast<float>(kbuf[j] * cg * (static_cast<double>(p) - sc.ybar));
-      }
-    }
-    XPG_STAMP(4)
-    lds_barrier();
+    // ---- poll, g and the G tables in one phase, within 16-lane groups (no barrier between):
+    // lane (grp, vv) owns table entry G[grp][vv]; its row is j = 4 grp + (vv & 3) and it polls
+    // slices q = vv >> 2 and q + 4 of that row (P <= 8); two xor-shuffles sum the 4 lanes of a
+    // row (the same tree in every workgroup, so every workgroup derives the same g), and the
+    // entry adds the g of its group's rows selected by the bits of vv (row order 0..3).
     {
       const int ngrp = (B + 3) >> 2;
-      for (int e = tid; e < ngrp * 16; e += 1024) {
-        const int grp = e >> 4, vv = e & 15;
+      const double cg = 2.0 / (static_cast<double>(B) * sc.ksum);
+      for (int e = tid; e < ngrp * 16; e += 1024) {  // whole 16-lane groups per iteration
+        const int grp = e >> 4, vv = e & 15, b = vv & 3, qq = vv >> 2;
+        const int j = 4 * grp + b;
+        float s = 0.f;
+        if (j < B) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int q = qq + 4 * h;
+            if (q < P) {
+              const uint64_t* src = xs + q * (int64_t)batch + j;
+              uint64_t gr = ld64_sc1(src);
+              uint32_t n = 0;
+              while (static_cast<uint32_t>(gr >> 32) != tag) {
+                __builtin_amdgcn_s_sleep(1);
+                gr = ld64_sc1(src);
+                if (++n > kMcSpinLimit) {
+                  __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  break;
+                }
+              }
+              s += __uint_as_float(static_cast<uint32_t>(gr));
+            }
+          }
+        }
+        s += __shfl_xor(s, 4, 16);
+        s += __shfl_xor(s, 8, 16);
+        float g = 0.f;
+        if (j < B) {
+          if (part == 0 && qq == 0) p_hist[r0 + j] = s;
+          g = static_cast<float>(kbuf[j] * cg * (static_cast<double>(s) - sc.ybar));
+        }
         float acc = 0.f;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int j = 4 * grp + b;
-          acc += ((vv >> b) & 1) && j < B ? pg[j] : 0.f;
+        for (int bb = 0; bb < 4; ++bb) {
+          const float gb = __shfl(g, bb, 16);
+          acc += ((vv >> bb) & 1) ? gb : 0.f;
         }
         G[grp * kTabPitch + vv] = acc;
       }
     }
+    XPG_STAMP(4)
     lds_barrier();  // G and Cb(t) complete; Rb, kbuf free
     XPG_STAMP(5)
     if (t + 1 < nsteps) XPG_MC_ROWS_LOAD(t + 1)
