@@ -179,6 +179,123 @@ __global__ __launch_bounds__(256) void k_shapley(uint64_t seed, int64_t row_offs
   }
 }
 
+// ------------------------------------------------------------------ community-aware masks
+// Device restatement of the community sampler (masks.py:81-194 + pathways.py:234-385): the
+// host lays out one block per community in length-descending order, blocks[b] = {row_start,
+// size, size_internal, own, off}: `own` is the community whose members get internal random
+// bits in every row of the block (masks.py:330), `off` the community column the reference
+// switches off in the external coalitions (it passes the sorted position, masks.py:168).
+// Row k >= size_internal of a block is an external coalition: the first h = ext/2 rows draw
+// community flags, the next h are their complements (antithetic, pathways.py:267-271), an odd
+// ext adds one more random row (:273-281); a lone external row with no flag on gets one other
+// community switched on (activate_dead_mask — with h >= 1 a pair can never be all-off).  The
+// active communities' members are switched on, the own members overwritten by the internal bits.
+// Row shuffle (masks.py:380): a seeded Feistel bijection of [0, 4^hb) cycle-walked into
+// [0, src_rows).  Every draw is a Philox word keyed by (block, row, word), so rows regenerate
+// independently of the launch shape.
+constexpr int kCommMaxWords = 1024;  // up to 32,768 communities (flag bitset in LDS)
+
+__device__ __forceinline__ uint32_t comm_mix(uint32_t x, uint32_t k) {
+  x ^= k;
+  x *= 0x9E3779B1u;
+  x ^= x >> 16;
+  x *= 0x85EBCA77u;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ uint32_t comm_permute(uint32_t x, uint32_t n, int hb, uint32_t k0, uint32_t k1) {
+  const uint32_t m = (1u << hb) - 1u;  // hb <= 16
+  do {  // terminates: x's cycle under the bijection contains the start, which is < n
+    uint32_t L = x >> hb, R = x & m;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t t = L ^ (comm_mix(R, ((i & 1) ? k1 : k0) + 0x632BE5ABu * i) & m);
+      L = R;
+      R = t;
+    }
+    x = (L << hb) | R;
+  } while (x >= n);
+  return x;
+}
+
+__global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t rows, int64_t cols, int words,
+                                                     int n_comm, const int32_t* __restrict__ blocks,
+                                                     int n_blocks, uint32_t src_rows, int hb, int shuffle,
+                                                     const int32_t* __restrict__ col_ptr,
+                                                     const int32_t* __restrict__ col_comm,
+                                                     uint32_t* __restrict__ bits, int32_t* __restrict__ prow) {
+  __shared__ uint32_t flags[kCommMaxWords];
+  __shared__ int sh_b, sh_any;
+  const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  const int fw = (n_comm + 31) >> 5;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const uint32_t src =
+        shuffle ? comm_permute(static_cast<uint32_t>(r), src_rows, hb, k0 ^ 0x5EED1234u, k1 ^ 0x0F00D321u)
+                : static_cast<uint32_t>(r);
+    if (threadIdx.x == 0) {  // last block whose row_start <= src
+      int lo = 0, hi = n_blocks - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (static_cast<uint32_t>(blocks[mid * 5]) <= src) lo = mid;
+        else hi = mid - 1;
+      }
+      sh_b = lo;
+      sh_any = 0;
+    }
+    __syncthreads();
+    const int b = sh_b;
+    const int* blk = blocks + b * 5;
+    const int size_int = blk[2], own = blk[3], off = blk[4];
+    const int h = (blk[1] - size_int) >> 1;
+    const int k = static_cast<int>(src) - blk[0] - size_int;  // < 0: internal-only row
+    for (int w = threadIdx.x; w < fw; w += blockDim.x) {
+      uint32_t v = 0u;
+      if (k >= 0) {
+        const int kk = k < h ? k : (k < 2 * h ? k - h : 2 * h);
+        v = philox4x32_10(make_uint4(static_cast<uint32_t>(w), static_cast<uint32_t>(b), static_cast<uint32_t>(kk),
+                                     0x434F4D31u), k0, k1).x;
+        if (k >= h && k < 2 * h) v = ~v;
+        if (w == fw - 1 && (n_comm & 31)) v &= (1u << (n_comm & 31)) - 1u;
+        if (w == (off >> 5)) v &= ~(1u << (off & 31));
+        if (v) sh_any = 1;
+      }
+      flags[w] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && k >= 0 && h == 0 && !sh_any && n_comm > 1) {
+      uint32_t pick = philox4x32_10(make_uint4(0u, static_cast<uint32_t>(b), static_cast<uint32_t>(k), 0x44454144u),
+                                    k0, k1).x % static_cast<uint32_t>(n_comm - 1);
+      if (static_cast<int>(pick) >= off) ++pick;
+      flags[pick >> 5] |= 1u << (pick & 31);
+    }
+    __syncthreads();
+    for (int w = threadIdx.x; w < words; w += blockDim.x) {
+      const uint32_t inner = philox4x32_10(make_uint4(static_cast<uint32_t>(w), src, 0u, 0x494E5431u), k0, k1).x;
+      const int64_t c0 = static_cast<int64_t>(w) * 32;
+      const int n = cols - c0 < 32 ? static_cast<int>(cols - c0) : 32;
+      uint32_t out = 0u;
+      for (int t = 0; t < n; ++t) {
+        int i = col_ptr[c0 + t];
+        const int e = col_ptr[c0 + t + 1];
+        uint32_t on = 0u;
+        bool mine = false;
+        for (; i < e; ++i) {
+          const int c = col_comm[i];
+          if (c == own) mine = true;
+          else on |= (flags[c >> 5] >> (c & 31)) & 1u;
+        }
+        out |= (mine ? ((inner >> t) & 1u) : on) << t;
+      }
+      bits[r * words + w] = out;
+    }
+    if (prow && threadIdx.x == 0) prow[r] = own;
+    __syncthreads();
+  }
+}
+
 __global__ void k_edge_keep(const uint32_t* __restrict__ bits, int64_t rows, int words,
                             const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                             int64_t n_edges, uint8_t* __restrict__ keep) {
@@ -3548,6 +3665,25 @@ int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, i
   if (rows == 0) return XPG_OK;
   XPG_HIP(hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)rows, S(stream)));
   return launch_shapley(seed, row_offset, rows, cols, bits, counts, S(stream));
+}
+
+int xpg_sample_communities(uint64_t seed, int64_t rows, int64_t cols, int32_t n_comm, const int32_t* blocks,
+                           int32_t n_blocks, int64_t src_rows, int32_t shuffle, const int32_t* col_ptr,
+                           const int32_t* col_comm, uint32_t* bits, int32_t* prow, xpg_stream_t stream) {
+  XPG_REQ(cols > 0 && rows >= 0 && n_comm > 0 && n_comm <= 32 * kCommMaxWords && n_blocks > 0 &&
+              n_blocks <= n_comm && src_rows >= rows && src_rows < (int64_t(1) << 31) && blocks && col_ptr &&
+              col_comm && bits,
+          "communities: bad shape");
+  if (rows == 0) return XPG_OK;
+  int nb = 1;  // bit length of src_rows - 1
+  while ((int64_t(1) << nb) < src_rows) ++nb;
+  const int hb = (nb + 1) / 2;
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(rows, 65536));
+  hipLaunchKernelGGL(k_communities, dim3(grid), dim3(256), 0, S(stream), seed, rows, cols, words_of(cols), n_comm,
+                     blocks, n_blocks, static_cast<uint32_t>(src_rows), hb, shuffle ? 1 : 0, col_ptr, col_comm,
+                     bits, prow);
+  XPG_LAUNCHED();
+  return XPG_OK;
 }
 
 int xpg_edge_keep(const uint32_t* bits, int64_t rows, int64_t cols, const int32_t* src, const int32_t* dst,

@@ -66,6 +66,42 @@ def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0,
     return bits, counts
 
 
+def community_columns(communities, cols):
+    """Column -> community CSR (int32 col_ptr [cols+1], col_comm [nnz]) of a community list."""
+    lens = np.array([len(c) for c in communities], dtype=np.int64)
+    members = (np.concatenate([np.asarray(c, dtype=np.int64) for c in communities])
+               if lens.sum() else np.zeros(0, dtype=np.int64))
+    assert members.size == 0 or (members.min() >= 0 and members.max() < cols), \
+        "community member outside the mask columns"
+    comm = np.repeat(np.arange(len(communities), dtype=np.int64), lens)
+    order = np.argsort(members, kind="stable")
+    col_ptr = np.zeros(cols + 1, dtype=np.int64)
+    np.cumsum(np.bincount(members, minlength=cols), out=col_ptr[1:])
+    return (torch.from_numpy(col_ptr.astype(np.int32)),
+            torch.from_numpy(comm[order].astype(np.int32)))
+
+
+def sample_communities(seed: int, plan, communities, cols: int, device, columns=None):
+    """Device community masks (masks.py:81-194, pathways.py:234-385).
+
+    plan = Mask.community_plan(); columns = community_columns(communities, cols) (reused across
+    repeats when given).  Returns (row bits int32 [rows, words], pathway_rows int32 [rows])."""
+    blocks, src_rows, rows, shuffle = plan
+    dev = torch.device(device)
+    col_ptr, col_comm = columns if columns is not None else community_columns(communities, cols)
+    blocks = blocks.to(dev, torch.int32).contiguous()
+    col_ptr = col_ptr.to(dev, torch.int32).contiguous()
+    col_comm = col_comm.to(dev, torch.int32).contiguous()
+    if col_comm.numel() == 0:
+        col_comm = torch.zeros(1, dtype=torch.int32, device=dev)
+    bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=dev)
+    prow = torch.empty(rows, dtype=torch.int32, device=dev)
+    call("xpg_sample_communities", ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), rows, cols,
+         len(communities), ptr(blocks), blocks.shape[0], src_rows, int(bool(shuffle)),
+         ptr(col_ptr), ptr(col_comm), ptr(bits), ptr(prow), _lib.stream_of(dev))
+    return bits, prow
+
+
 def edge_keep(bits, cols, src, dst):
     """data.py:390-451 edge mask: [rows * n_edges] bool, copy-major."""
     _lib.require_device(bits, "bits")

@@ -202,11 +202,23 @@ class Explainer:
         # RNG order (mask_generator -> LinearRegression init -> DataLoader seed, per repeat);
         # then run all repeats' forward / KernelSHAP / surrogate fits as batched launches.
         bits_list, w0_list, masks = [], [], []
+        on_device = sampler == "device" and "edge" not in self.problem
+        if on_device and c["sub_pw_inds"] is not None:
+            # device community sampler: the block plan and column -> community CSR are
+            # repeat-invariant; each repeat draws a new seed (masks.py:262-397)
+            cmask = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params, self.problem)
+            cplan = cmask.community_plan()
+            ccols = engine.community_columns(c["sub_pw_inds"], S)
         for _ in range(times):
-            if sampler == "device" and c["sub_pw_inds"] is None and "edge" not in self.problem:
+            if on_device and c["sub_pw_inds"] is None:
                 R = int(self.params["interpret_samples"] * epochs)
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
                 bits_list.append(engine.sample_shapley(seed, R, S, device))
+                masks.append(None)
+            elif on_device:
+                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+                bits_list.append(engine.sample_communities(seed, cplan, c["sub_pw_inds"], S,
+                                                           device, ccols)[0])
                 masks.append(None)
             else:
                 mask, _ = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,

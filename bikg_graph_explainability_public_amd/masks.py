@@ -6,9 +6,13 @@ Two samplers share one output contract (bool [R, S] rows + per-row community ind
   CPU generator in the reference's exact call order — per community in length-descending order:
   internal randint, external antithetic randint (+ extra row), optional dead-mask randperm; then
   the row shuffle randperm — so masks are bit-identical to the reference CPU path for the same
-  RNG state (tests/test_masks_golden.py).  Rows are then bit-packed on the device.
-* device (`"device"`): counter-based Philox Shapley bits generated directly in HBM by the HIP
-  sampler (engine.sample_shapley) — same distribution, no host work; used for throughput.
+  RNG state (tests/test_host_cpu.py::test_compat_sampler_reproduces_reference_masks).  Rows
+  are then bit-packed on the device.
+* device (`"device"`): counter-based Philox bits generated directly in HBM by the HIP samplers
+  — same distribution, no host work; used for throughput.  Without communities:
+  engine.sample_shapley; with communities: engine.sample_communities over the block plan of
+  `Mask.community_plan` (same block sizes, antithetic coalitions, dead-mask activation and
+  own-community internal bits; the row shuffle is a seeded bijection instead of randperm).
 """
 import itertools
 import math
@@ -52,15 +56,44 @@ class Mask(Data):
         return self.feat.device
 
     @staticmethod
-    def get_internal_mask(pathway, len_pathways, total_size, device):
-        """masks.py:81-136 — rows proportional to the community size; random member bits."""
-        fraction = len(pathway) / torch.sum(len_pathways)
+    def internal_sizes(n_members, len_pathways, total_size):
+        """masks.py:98-118 — (block rows, internal-only rows) of one community."""
+        fraction = n_members / torch.sum(len_pathways)
         size = math.ceil(fraction * total_size)
         size_internal = math.ceil(fraction * size)
         if size_internal < 3:
             size_internal, size = 1, 2
+        return size, size_internal
+
+    @staticmethod
+    def get_internal_mask(pathway, len_pathways, total_size, device):
+        """masks.py:81-136 — rows proportional to the community size; random member bits."""
+        size, size_internal = Mask.internal_sizes(len(pathway), len_pathways, total_size)
         internal = torch.randint(0, 2, (size, len(pathway)), dtype=torch.bool)
         return internal.to(device), size_internal
+
+    def community_plan(self):
+        """Host plan of the device community sampler (engine.sample_communities): the block
+        loop of `generate` without its random draws.  Returns (blocks int32 [P', 5] =
+        {row_start, size, size_internal, own, off}, src_rows, out_rows, shuffle) — the
+        reference truncates to the `total` rows of the largest communities instead of
+        shuffling when S > 4000 (masks.py:340-380)."""
+        n_perturbs, epochs = self.assertions_mask_generator(self.params)
+        total = n_perturbs * epochs
+        S = self.element_count()
+        lens = torch.tensor([len(p) for p in self.pathways])
+        order = torch.argsort(lens, descending=True)
+        blocks, start = [], 0
+        for e in range(order.shape[0]):
+            size, size_internal = self.internal_sizes(len(self.pathways[order[e]]), lens, total)
+            blocks.append((start, size, size_internal, int(order[e]), e))
+            start += size
+            if start - size > total and S > 4000:
+                break
+        out_rows, shuffle = start, True
+        if S > 4000 and start > total:
+            out_rows, shuffle = int(total), False
+        return torch.tensor(blocks, dtype=torch.int32), start, out_rows, shuffle
 
     def get_external_indices(self, full_mask, ind_pathway, size_internal):
         """masks.py:138-194 — external coalitions for rows size_internal..end.  Column

@@ -14,6 +14,9 @@
  *   xpg_pack_masks / xpg_unpack_masks  — bool mask batches handed between masks.py and
  *                                        wlm.py (DataLoader batches, masks.py:197-229)
  *   xpg_sample_shapley                 — Mask.shapley_mask           masks.py:231-260
+ *   xpg_sample_communities             — Mask.get_internal_mask / get_external_indices +
+ *                                        Pathways.mask_generator (masks.py:81-194,
+ *                                        pathways.py:234-385)
  *   xpg_edge_keep                      — Data.build_edge_mask        data.py:390-451
  *   xpg_popcount_rows + xpg_shap_kernel— Kernel.compute             kernels.py:115-174
  *   xpg_masked_forward                 — Data.perturbator + Model.infer + extract_node_edge_output
@@ -36,7 +39,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 7
+#define XPG_ABI_VERSION 8
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -66,6 +69,18 @@ int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t 
  * accumulated while sampling so KernelSHAP needs no second pass over the bits. */
 int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
                               uint32_t* bits, int32_t* counts, xpg_stream_t stream);
+/* Community-aware masks — replaces Mask.get_internal_mask / get_external_indices and
+ * Pathways.mask_generator / activate_dead_mask / pathway_mask2node_mask (masks.py:81-194,
+ * pathways.py:234-385) plus the row shuffle (masks.py:375-380), generated in HBM.
+ * blocks (device, int32 [n_blocks][5]) = {row_start, size, size_internal, own, off} per
+ * community in length-descending order (the host plan, masks.py:309-340); col_ptr / col_comm
+ * (device, int32 [cols+1] / [nnz]) = the communities each column belongs to.  Output row r is
+ * source row perm(r) (shuffle != 0; a seeded bijection of [0, src_rows)) or r (shuffle == 0,
+ * the S > 4000 truncation branch); prow (nullable) gets the row's community (pathway_rows). */
+int xpg_sample_communities(uint64_t seed, int64_t rows, int64_t cols, int32_t n_comm,
+                           const int32_t* blocks, int32_t n_blocks, int64_t src_rows,
+                           int32_t shuffle, const int32_t* col_ptr, const int32_t* col_comm,
+                           uint32_t* bits, int32_t* prow, xpg_stream_t stream);
 
 /* ---------------------------------------------------------------- perturbation */
 /* keep[b*n_edges + e] = bit(b, src[e]) & bit(b, dst[e])   (data.py:420-449) */

@@ -166,3 +166,50 @@ def test_engine_refuses_cpu_tensors():
     from bikg_graph_explainability_public_amd import engine
     with pytest.raises(_lib.NativeLibraryError):
         engine.pack_masks(torch.zeros((2, 3), dtype=torch.bool))
+
+
+def _plan_mask(S, pathways, samples, epochs=2):
+    return Mask(torch.zeros((S, 1)), torch.zeros((2, 0), dtype=torch.long), pathways,
+                {"interpret_samples": samples, "epochs": epochs}, "node_prediction")
+
+
+@pytest.mark.parametrize("S, lens, samples", [
+    (36, None, 20),                                  # the test_run communities (golden case)
+    (300, [40, 7, 2, 1, 25, 60, 3], 100),            # tiny communities: size_internal < 3
+    (5000, [900, 700, 40, 30, 20, 10, 5], 30),       # S > 4000: truncated to the total rows
+])
+def test_community_plan_matches_compat_blocks(S, lens, samples):
+    """Mask.community_plan (the device sampler's host plan) has the compat sampler's block
+    sizes, community order and row count (masks.py:309-380)."""
+    if lens is None:
+        exp, z, meta = build_explainer("test_run")
+        ctx = exp.prepare(meta["element"], torch.device("cpu"))
+        pathways, S = ctx["sub_pw_inds"], ctx["S"]
+        samples = exp.params["interpret_samples"]
+    else:
+        rng = np.random.default_rng(S)
+        perm = rng.permutation(S)
+        pathways, o = [], 0
+        for n in lens:
+            pathways.append(sorted(perm[o:o + n].tolist()))
+            o += n
+    torch.manual_seed(0)
+    mask, prow = _plan_mask(S, [list(p) for p in pathways], samples).generate()
+    blocks, src_rows, out_rows, shuffle = _plan_mask(S, [list(p) for p in pathways],
+                                                     samples).community_plan()
+    b = blocks.numpy()
+    assert out_rows == mask.shape[0] and (b[:, 0] == np.concatenate([[0], np.cumsum(b[:-1, 1])])).all()
+    assert src_rows == int(b[:, 1].sum()) and shuffle == (S <= 4000 or src_rows <= samples * 2)
+    assert (b[:, 2] <= b[:, 1]).all() and sorted(b[:, 4].tolist()) == list(range(len(b)))
+    counts = np.bincount(prow.numpy(), minlength=len(pathways))
+    if shuffle:
+        assert np.array_equal(counts[b[:, 3]], b[:, 1])
+    else:  # truncation keeps the largest communities' rows first
+        assert counts.sum() == out_rows and set(np.flatnonzero(counts)) <= set(b[:, 3].tolist())
+
+
+def test_community_columns_csr():
+    from bikg_graph_explainability_public_amd.engine import community_columns
+    ptr_, comm = community_columns([[0, 3, 4], [4, 5], [1]], 7)
+    assert ptr_.tolist() == [0, 1, 2, 2, 3, 5, 6, 6]
+    assert comm.tolist() == [0, 2, 0, 0, 1, 1]
