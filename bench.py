@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--full-graph-rows", type=int, default=64,
                    help="regime (ii): mask rows of the c3-shaped full-graph forward (0 = skip)")
     p.add_argument("--no-hetero", action="store_true", help="skip the c4 multi-type section")
+    p.add_argument("--no-communities", action="store_true",
+                   help="skip the c2 community-sampler section")
     p.add_argument("--no-graph-prediction", action="store_true",
                    help="skip the c3 graph_prediction per-query pipeline section")
     return p.parse_args()
@@ -443,6 +445,56 @@ def hetero_c4_section(args, dev):
             "reference_loop_gpu_samples_per_s": loop_rate}
 
 
+def communities_section(args, dev, plan, sub_feat, sub_ei, reps=10):
+    """c2 with 20 random communities over the subgraph (SURVEY.md §8d c5-style communities):
+    the device community sampler (k_communities) inside the full repeat pipeline, and the
+    compat CPU sampler (the reference's masks.py:262-397 algorithm and RNG order) beside it."""
+    from bikg_graph_explainability_public_amd import engine
+    from bikg_graph_explainability_public_amd.masks import Mask
+    S = plan.cols
+    rng = np.random.default_rng(20)
+    cuts = np.sort(rng.choice(np.arange(1, S), 19, replace=False))
+    pathways = [c.tolist() for c in np.split(rng.permutation(S), cuts)]
+    params = {"interpret_samples": args.interpret_samples, "epochs": args.epochs}
+    m = Mask(sub_feat, sub_ei, pathways, params, "node_prediction")
+    cplan = m.community_plan()
+    tabs = engine.community_tables(cplan, pathways, S, dev)
+    R = cplan[2]
+    batch = R // args.epochs
+    w0 = torch.zeros((1, S), device=dev)
+    fit = {"lr": 0.01, "l1_lambda": 1e-4}
+    stream = torch.cuda.current_stream()
+
+    def rep(i):
+        bits, _ = engine.sample_communities(4000 + i, cplan, pathways, S, dev, tables=tabs)
+        y = plan.forward(bits)[:, 0]
+        k = engine.shap_kernel(bits, S)
+        return engine.wlm_fit(bits.view(1, R, -1), S, batch, y.view(1, R), k.view(1, R), w0, fit)
+
+    rep(0)
+    torch.cuda.synchronize()
+    a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    a.record(stream)
+    for i in range(reps):
+        engine.sample_communities(5000 + i, cplan, pathways, S, dev, tables=tabs)
+    b.record(stream)
+    for i in range(reps):
+        rep(i)
+    c.record(stream)
+    torch.cuda.synchronize()
+    samp_ms = a.elapsed_time(b) / reps
+    rep_ms = b.elapsed_time(c) / reps
+    t0 = time.perf_counter()
+    Mask(sub_feat.cpu(), sub_ei.cpu(), [list(p) for p in pathways], params,
+         "node_prediction").generate()
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    return {"workload": f"c2 subgraph ({S} cols), 20 random communities, {R} rows per repeat",
+            "samples_per_s": R / (rep_ms * 1e-3), "ms_per_repeat": rep_ms,
+            "sampler_ms": samp_ms,
+            "sampler_write_GBps": R * ((S + 31) // 32) * 4 / (samp_ms * 1e-3) / 1e9,
+            "cpu_compat_sampler_ms": cpu_ms, "cpu_sampler_cores": torch.get_num_threads()}
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -558,6 +610,7 @@ def main():
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, arch, sub_feat, sub_ei, q)
         if world == 1:
+            comm = None if args.no_communities else communities_section(args, dev, plan, sub_feat, sub_ei)
             del plan
             torch.cuda.empty_cache()
             regimes = {}
@@ -570,6 +623,8 @@ def main():
             if not args.no_hetero:
                 regimes["hetero_c4"] = hetero_c4_section(args, dev)
                 torch.cuda.empty_cache()
+            if comm is not None:
+                regimes["communities_c2"] = comm
             if regimes:
                 line["regimes"] = regimes
         print(json.dumps(line), flush=True)

@@ -221,78 +221,131 @@ __device__ uint32_t comm_permute(uint32_t x, uint32_t n, int hb, uint32_t k0, ui
   return x;
 }
 
+// One wave per output row (4 rows per 256-thread workgroup).  SMALL (<= 64 communities): the
+// row's community flags live in one 64-bit register (word w drawn by lane w, shuffled to all);
+// else in a per-wave LDS bitset.  Columns are lane-parallel (lane = column within a 64-column
+// slice): each lane looks up its column's communities, the slice's bits come out of one ballot,
+// and lane j keeps slice j's ballot until 64 slices are ready, then they are stored together.
+// STAGED (cols <= kCommStageCols): each workgroup first stages every column's community as one
+// int16 in LDS (-1: none, -2: several -> the CSR in global memory), so the per-slice lookups are
+// LDS reads instead of two dependent L2 loads; the block plan is staged beside it.
+constexpr int kCommStageCols = 16384;
+template <bool SMALL, bool STAGED>
 __global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t rows, int64_t cols, int words,
                                                      int n_comm, const int32_t* __restrict__ blocks,
                                                      int n_blocks, uint32_t src_rows, int hb, int shuffle,
                                                      const int32_t* __restrict__ col_ptr,
                                                      const int32_t* __restrict__ col_comm,
                                                      uint32_t* __restrict__ bits, int32_t* __restrict__ prow) {
-  __shared__ uint32_t flags[kCommMaxWords];
-  __shared__ int sh_b, sh_any;
-  const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  // dynamic LDS, sized by the launcher: [4 x fw flag words (!SMALL)] [5 x n_blocks plan (STAGED)]
+  // [cols x int16 column community (STAGED)] — a few KB at subgraph sizes, so occupancy stays high
+  extern __shared__ uint32_t comm_lds[];
   const int fw = (n_comm + 31) >> 5;
-  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
-    const uint32_t src =
-        shuffle ? comm_permute(static_cast<uint32_t>(r), src_rows, hb, k0 ^ 0x5EED1234u, k1 ^ 0x0F00D321u)
-                : static_cast<uint32_t>(r);
-    if (threadIdx.x == 0) {  // last block whose row_start <= src
-      int lo = 0, hi = n_blocks - 1;
+  uint32_t* lflags = comm_lds;
+  int32_t* lblk = reinterpret_cast<int32_t*>(comm_lds + (SMALL ? 0 : 4 * fw));
+  int16_t* lone = reinterpret_cast<int16_t*>(lblk + (STAGED ? 5 * n_blocks : 0));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (STAGED) {
+    for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+      const int p0 = col_ptr[c], n = col_ptr[c + 1] - p0;
+      lone[c] = static_cast<int16_t>(n == 0 ? -1 : (n == 1 ? col_comm[p0] : -2));
+    }
+    for (int i = threadIdx.x; i < 5 * n_blocks; i += blockDim.x) lblk[i] = blocks[i];
+    __syncthreads();
+    blocks = lblk;
+  }
+  uint32_t* flags = lflags + (SMALL ? 0 : wv * fw);
+  const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  for (int64_t base = static_cast<int64_t>(blockIdx.x) * 4; base < rows; base += static_cast<int64_t>(gridDim.x) * 4) {
+    const int64_t r = base + wv;
+    const bool active = r < rows;  // inactive waves still reach every barrier
+    uint32_t src = 0u;
+    int b = 0;
+    if (active) {
+      src = shuffle ? comm_permute(static_cast<uint32_t>(r), src_rows, hb, k0 ^ 0x5EED1234u, k1 ^ 0x0F00D321u)
+                    : static_cast<uint32_t>(r);
+      int lo = 0, hi = n_blocks - 1;  // last block whose row_start <= src (wave-uniform)
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (static_cast<uint32_t>(blocks[mid * 5]) <= src) lo = mid;
         else hi = mid - 1;
       }
-      sh_b = lo;
-      sh_any = 0;
+      b = lo;
     }
-    __syncthreads();
-    const int b = sh_b;
     const int* blk = blocks + b * 5;
-    const int size_int = blk[2], own = blk[3], off = blk[4];
-    const int h = (blk[1] - size_int) >> 1;
-    const int k = static_cast<int>(src) - blk[0] - size_int;  // < 0: internal-only row
-    for (int w = threadIdx.x; w < fw; w += blockDim.x) {
+    const int size_int = active ? blk[2] : 0, own = active ? blk[3] : -1, off = active ? blk[4] : 0;
+    const int h = active ? (blk[1] - size_int) >> 1 : 0;
+    const int k = active ? static_cast<int>(src) - blk[0] - size_int : -1;  // < 0: internal-only row
+    // external coalition flags (antithetic pair / extra row), sorted-position column off
+    int any = 0;
+    uint64_t f64 = 0;
+    for (int w0 = 0; w0 < fw; w0 += 64) {
+      const int w = w0 + lane;
       uint32_t v = 0u;
-      if (k >= 0) {
+      if (k >= 0 && w < fw) {
         const int kk = k < h ? k : (k < 2 * h ? k - h : 2 * h);
         v = philox4x32_10(make_uint4(static_cast<uint32_t>(w), static_cast<uint32_t>(b), static_cast<uint32_t>(kk),
                                      0x434F4D31u), k0, k1).x;
         if (k >= h && k < 2 * h) v = ~v;
         if (w == fw - 1 && (n_comm & 31)) v &= (1u << (n_comm & 31)) - 1u;
         if (w == (off >> 5)) v &= ~(1u << (off & 31));
-        if (v) sh_any = 1;
       }
-      flags[w] = v;
+      any |= v != 0u;
+      if (SMALL) f64 = static_cast<uint64_t>(__shfl(v, 0, 64)) | (static_cast<uint64_t>(__shfl(v, 1, 64)) << 32);
+      else if (w < fw) flags[w] = v;
     }
-    __syncthreads();
-    if (threadIdx.x == 0 && k >= 0 && h == 0 && !sh_any && n_comm > 1) {
+    // activate_dead_mask: only a lone external row can be all-off (a pair never is)
+    int extra = -1;
+    if (k >= 0 && h == 0 && n_comm > 1 && !__any(any)) {
       uint32_t pick = philox4x32_10(make_uint4(0u, static_cast<uint32_t>(b), static_cast<uint32_t>(k), 0x44454144u),
                                     k0, k1).x % static_cast<uint32_t>(n_comm - 1);
       if (static_cast<int>(pick) >= off) ++pick;
-      flags[pick >> 5] |= 1u << (pick & 31);
+      extra = static_cast<int>(pick);
     }
-    __syncthreads();
-    for (int w = threadIdx.x; w < words; w += blockDim.x) {
-      const uint32_t inner = philox4x32_10(make_uint4(static_cast<uint32_t>(w), src, 0u, 0x494E5431u), k0, k1).x;
-      const int64_t c0 = static_cast<int64_t>(w) * 32;
-      const int n = cols - c0 < 32 ? static_cast<int>(cols - c0) : 32;
-      uint32_t out = 0u;
-      for (int t = 0; t < n; ++t) {
-        int i = col_ptr[c0 + t];
-        const int e = col_ptr[c0 + t + 1];
-        uint32_t on = 0u;
-        bool mine = false;
-        for (; i < e; ++i) {
-          const int c = col_comm[i];
-          if (c == own) mine = true;
-          else on |= (flags[c >> 5] >> (c & 31)) & 1u;
+    if (!SMALL) __syncthreads();
+    if (active) {
+      uint64_t keep = 0;
+      const int slices = static_cast<int>((cols + 63) >> 6);
+      uint32_t* dst = bits + r * words;
+      for (int sl = 0; sl < slices; ++sl) {
+        const int64_t c = static_cast<int64_t>(sl) * 64 + lane;
+        uint32_t bit = 0u;
+        const int one = (STAGED && c < cols) ? lone[c] : -2;
+        if (one >= 0) {
+          if (one == own) bit = (philox4x32_10(make_uint4(static_cast<uint32_t>(c >> 5), src, 0u, 0x494E5431u), k0, k1).x >> (c & 31)) & 1u;
+          else if (one == extra) bit = 1u;
+          else if (SMALL) bit = static_cast<uint32_t>(f64 >> one) & 1u;
+          else bit = (flags[one >> 5] >> (one & 31)) & 1u;
+        } else if (one == -2 && c < cols) {
+          int i = col_ptr[c];
+          const int e = col_ptr[c + 1];
+          bool mine = false;
+          for (; i < e; ++i) {
+            const int cc = col_comm[i];
+            if (cc == own) mine = true;
+            else if (cc == extra) bit = 1u;
+            else if (SMALL) bit |= static_cast<uint32_t>(f64 >> cc) & 1u;
+            else bit |= (flags[cc >> 5] >> (cc & 31)) & 1u;
+          }
+          if (mine) {
+            const uint32_t inner = philox4x32_10(make_uint4(static_cast<uint32_t>(c >> 5), src, 0u, 0x494E5431u), k0, k1).x;
+            bit = (inner >> (c & 31)) & 1u;
+          }
         }
-        out |= (mine ? ((inner >> t) & 1u) : on) << t;
+        const uint64_t bal = __ballot(bit);
+        if (lane == (sl & 63)) keep = bal;
+        if ((sl & 63) == 63 || sl == slices - 1) {
+          const int first = sl & ~63;
+          if (lane <= (sl & 63)) {
+            const int w = (first + lane) * 2;
+            dst[w] = static_cast<uint32_t>(keep);
+            if (w + 1 < words) dst[w + 1] = static_cast<uint32_t>(keep >> 32);
+          }
+        }
       }
-      bits[r * words + w] = out;
+      if (lane == 0 && prow) prow[r] = own;
     }
-    if (prow && threadIdx.x == 0) prow[r] = own;
-    __syncthreads();
+    if (!SMALL) __syncthreads();
   }
 }
 
@@ -3678,10 +3731,23 @@ int xpg_sample_communities(uint64_t seed, int64_t rows, int64_t cols, int32_t n_
   int nb = 1;  // bit length of src_rows - 1
   while ((int64_t(1) << nb) < src_rows) ++nb;
   const int hb = (nb + 1) / 2;
-  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(rows, 65536));
-  hipLaunchKernelGGL(k_communities, dim3(grid), dim3(256), 0, S(stream), seed, rows, cols, words_of(cols), n_comm,
-                     blocks, n_blocks, static_cast<uint32_t>(src_rows), hb, shuffle ? 1 : 0, col_ptr, col_comm,
-                     bits, prow);
+  const bool small = n_comm <= 64;
+  const size_t flag_bytes = small ? 0 : sizeof(uint32_t) * 4 * static_cast<size_t>((n_comm + 31) / 32);
+  const size_t stage_bytes = sizeof(int32_t) * 5 * static_cast<size_t>(n_blocks) + sizeof(int16_t) * static_cast<size_t>(cols);
+  const bool staged = cols <= kCommStageCols && flag_bytes + stage_bytes <= 64 * 1024;
+  const size_t lds = flag_bytes + (staged ? stage_bytes : 0);
+  const int64_t want = std::min<int64_t>(cdiv(rows, 4), staged ? 2048 : 65536);
+  const dim3 g(static_cast<unsigned>(want));
+#define XPG_COMM(SM, ST)                                                                                      \
+  hipLaunchKernelGGL((k_communities<SM, ST>), g, dim3(256), lds, S(stream), seed, rows, cols, words_of(cols), n_comm, \
+                     blocks, n_blocks, static_cast<uint32_t>(src_rows), hb, shuffle ? 1 : 0, col_ptr, col_comm, bits, \
+                     prow)
+  if (small) {
+    if (staged) XPG_COMM(true, true); else XPG_COMM(true, false);
+  } else {
+    if (staged) XPG_COMM(false, true); else XPG_COMM(false, false);
+  }
+#undef XPG_COMM
   XPG_LAUNCHED();
   return XPG_OK;
 }

@@ -81,23 +81,34 @@ def community_columns(communities, cols):
             torch.from_numpy(comm[order].astype(np.int32)))
 
 
-def sample_communities(seed: int, plan, communities, cols: int, device, columns=None):
-    """Device community masks (masks.py:81-194, pathways.py:234-385; DESIGN.md §4).
-
-    plan = Mask.community_plan(); columns = community_columns(communities, cols) (reused across
-    repeats when given).  Returns (row bits int32 [rows, words], pathway_rows int32 [rows])."""
+def community_tables(plan, communities, cols: int, device, columns=None):
+    """Device copies of a community plan (Mask.community_plan) and its column -> community CSR,
+    uploaded once and reused by every repeat's `sample_communities(..., tables=...)`."""
     blocks, src_rows, rows, shuffle = plan
     dev = torch.device(device)
     col_ptr, col_comm = columns if columns is not None else community_columns(communities, cols)
-    blocks = blocks.to(dev, torch.int32).contiguous()
-    col_ptr = col_ptr.to(dev, torch.int32).contiguous()
-    col_comm = col_comm.to(dev, torch.int32).contiguous()
     if col_comm.numel() == 0:
-        col_comm = torch.zeros(1, dtype=torch.int32, device=dev)
+        col_comm = torch.zeros(1, dtype=torch.int32)
+    up = lambda t: t.to(dev, torch.int32).contiguous()
+    return (up(blocks), up(col_ptr), up(col_comm), int(src_rows), int(rows), bool(shuffle),
+            len(communities), int(cols))
+
+
+def sample_communities(seed: int, plan, communities, cols: int, device, columns=None,
+                       tables=None):
+    """Device community masks (masks.py:81-194, pathways.py:234-385; DESIGN.md §4).
+
+    plan = Mask.community_plan(); columns = community_columns(communities, cols); tables =
+    community_tables(...) (skips the per-call uploads).  Returns (row bits int32 [rows, words],
+    pathway_rows int32 [rows])."""
+    if tables is None:
+        tables = community_tables(plan, communities, cols, device, columns)
+    blocks, col_ptr, col_comm, src_rows, rows, shuffle, n_comm, cols = tables
+    dev = blocks.device
     bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=dev)
     prow = torch.empty(rows, dtype=torch.int32, device=dev)
     call("xpg_sample_communities", ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), rows, cols,
-         len(communities), ptr(blocks), blocks.shape[0], src_rows, int(bool(shuffle)),
+         n_comm, ptr(blocks), blocks.shape[0], src_rows, int(shuffle),
          ptr(col_ptr), ptr(col_comm), ptr(bits), ptr(prow), _lib.stream_of(dev))
     return bits, prow
 

@@ -208,7 +208,7 @@ class Explainer:
             # repeat-invariant; each repeat draws a new seed (masks.py:262-397)
             cmask = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params, self.problem)
             cplan = cmask.community_plan()
-            ccols = engine.community_columns(c["sub_pw_inds"], S)
+            ctabs = engine.community_tables(cplan, c["sub_pw_inds"], S, device)
         for _ in range(times):
             if on_device and c["sub_pw_inds"] is None:
                 R = int(self.params["interpret_samples"] * epochs)
@@ -218,7 +218,7 @@ class Explainer:
             elif on_device:
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
                 bits_list.append(engine.sample_communities(seed, cplan, c["sub_pw_inds"], S,
-                                                           device, ccols)[0])
+                                                           device, tables=ctabs)[0])
                 masks.append(None)
             else:
                 mask, _ = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,

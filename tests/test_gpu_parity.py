@@ -116,7 +116,9 @@ def _community_case(S, lens, samples, seed=0):
 
 @pytest.mark.parametrize("S, lens, samples", [(300, [40, 7, 2, 1, 25, 60, 3], 100),
                                               (3000, [1000, 700, 33, 300, 5], 2000),
-                                              (70, [70], 10)])
+                                              (70, [70], 10),
+                                              (4000, [20] * 100 + [7] * 50, 500),  # LDS flags
+                                              (20000, [5000, 3000, 40, 7], 200)])  # unstaged
 def test_community_sampler_structure(S, lens, samples):
     """Device community sampler (masks.py:81-194, pathways.py:234-385), unshuffled: every block
     row has the reference's structure — uncovered columns off; internal rows touch only the own
