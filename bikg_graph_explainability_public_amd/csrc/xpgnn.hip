@@ -307,12 +307,16 @@ __global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t rows
       uint64_t keep = 0;
       const int slices = static_cast<int>((cols + 63) >> 6);
       uint32_t* dst = bits + r * words;
+      uint32_t inner = 0u;  // internal-bit words 2*(sl & ~31) .. +63, one Philox word per lane
       for (int sl = 0; sl < slices; ++sl) {
         const int64_t c = static_cast<int64_t>(sl) * 64 + lane;
+        if ((sl & 31) == 0)
+          inner = philox4x32_10(make_uint4(static_cast<uint32_t>((sl >> 5) * 64 + lane), src, 0u, 0x494E5431u), k0, k1).x;
+        const uint32_t iw = __shfl(inner, ((sl & 31) << 1) + (lane >> 5), 64);  // word c >> 5
         uint32_t bit = 0u;
         const int one = (STAGED && c < cols) ? lone[c] : -2;
         if (one >= 0) {
-          if (one == own) bit = (philox4x32_10(make_uint4(static_cast<uint32_t>(c >> 5), src, 0u, 0x494E5431u), k0, k1).x >> (c & 31)) & 1u;
+          if (one == own) bit = (iw >> (c & 31)) & 1u;
           else if (one == extra) bit = 1u;
           else if (SMALL) bit = static_cast<uint32_t>(f64 >> one) & 1u;
           else bit = (flags[one >> 5] >> (one & 31)) & 1u;
@@ -327,10 +331,7 @@ __global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t rows
             else if (SMALL) bit |= static_cast<uint32_t>(f64 >> cc) & 1u;
             else bit |= (flags[cc >> 5] >> (cc & 31)) & 1u;
           }
-          if (mine) {
-            const uint32_t inner = philox4x32_10(make_uint4(static_cast<uint32_t>(c >> 5), src, 0u, 0x494E5431u), k0, k1).x;
-            bit = (inner >> (c & 31)) & 1u;
-          }
+          if (mine) bit = (iw >> (c & 31)) & 1u;
         }
         const uint64_t bal = __ballot(bit);
         if (lane == (sl & 63)) keep = bal;
