@@ -290,6 +290,79 @@ class Explainer:
                          "sub_ind": sub_ind, "plan": plan, "weights": config_vals}
         return config_val_df, pathway_df
 
+    def run_queries(self, elements, times=1):
+        """Several graph_prediction queries over ONE mask set per repeat.
+
+        The reference explains one element per `run` (explainer.py:316-546) and draws new masks
+        each time.  In graph_prediction every query perturbs the same S = N columns
+        (explainer.py:427-447), so here each repeat's masks are drawn once, one masked forward
+        produces every query's logit per row (a multi-query ForwardPlan), KernelSHAP runs once,
+        and each query gets its own surrogate fits.  RNG order per repeat: masks, then one
+        LinearRegression init per query, then the DataLoader seed draw — with one query this is
+        exactly `run`'s order, so `run_queries([e]) == [run(e)]`.  Returns [(config_val_df,
+        pathway_df)] in `elements` order.  Engine-compilable single-node-type archs only."""
+        assert "graph" in self.problem, \
+            "run_queries shares one mask set across queries: graph_prediction problems only"
+        if not torch.cuda.is_available():
+            raise _lib.NativeLibraryError("Explainer.run_queries needs an MI355X (HIP) device; "
+                                          "there is no CPU fallback")
+        _lib.load()
+        device = torch.device("cuda", torch.cuda.current_device())
+        if times == 1:
+            set_seed(self.params["seed"])
+        self.arch = self.arch.to(device).eval()
+        c = self.prepare(elements[0], device)
+        inds = [c["sub_ind"]] + [self.prepare(e, device)["sub_ind"] for e in elements[1:]]
+        sub_feat, sub_ei, S = c["sub_feat"], c["sub_ei"], c["S"]
+        geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
+        plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, inds, *geo)
+        assert plan is not None and not getattr(plan, "multi_type", False), \
+            "run_queries needs an engine-compilable single-node-type architecture"
+        if self.params.get("verify_arch", True):
+            ok, err = pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, inds[0], *geo)
+            assert ok, f"compiled arch disagrees with its torch forward (max err {err:.3g})"
+        Q = len(inds)
+        assert len(set(inds)) == Q, "run_queries: duplicate query elements"
+        sampler = self.params.get("mask_sampler", "compat")
+        _, epochs = Mask.assertions_mask_generator(self.params)
+        if sampler == "device" and c["sub_pw_inds"] is not None:
+            cmask = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params, self.problem)
+            cplan = cmask.community_plan()
+            ctabs = engine.community_tables(cplan, c["sub_pw_inds"], S, device)
+        bits_list, w0 = [], [[] for _ in range(Q)]
+        for _ in range(times):
+            if sampler == "device":
+                R = int(self.params["interpret_samples"] * epochs)
+                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+                bits_list.append(engine.sample_shapley(seed, R, S, device)
+                                 if c["sub_pw_inds"] is None else
+                                 engine.sample_communities(seed, cplan, c["sub_pw_inds"], S,
+                                                           device, tables=ctabs)[0])
+            else:
+                mask, _ = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,
+                               self.problem).generate()
+                bits_list.append(engine.pack_masks(mask.to(device)))
+            for q in range(Q):
+                w0[q].append(LinearRegression(S).layer.weight.detach().reshape(-1))
+            dataloader_seed_draw()
+        R = bits_list[0].shape[0]
+        batch = R // epochs
+        bits = torch.stack(bits_list)                       # [times, R, W]
+        flat = bits.reshape(times * R, -1)
+        y = plan.forward(flat).reshape(times, R, -1)        # [times, R, >= Q]
+        kern = engine.shap_kernel(flat, S).reshape(times, R)
+        out = []
+        for q in range(Q):
+            w, _, _, _, _ = engine.wlm_fit(bits, S, batch, y[:, :, q].contiguous(), kern,
+                                           torch.stack(w0[q]), self.params)
+            mean, std = self.weight_stacking([w[i] for i in range(times)])
+            df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
+            pdf = None
+            if c["has_pathways"]:
+                pdf = Pathways(c["sub_pw"], c["sub_pw_names"]).aggregate(mean, c["sub_pw_inds"])
+            out.append((df, pdf))
+        return out
+
 
 def _to_device(x, device):
     if isinstance(x, dict):
