@@ -495,6 +495,46 @@ def communities_section(args, dev, plan, sub_feat, sub_ei, reps=10):
             "cpu_compat_sampler_ms": cpu_ms, "cpu_sampler_cores": torch.get_num_threads()}
 
 
+def graph_queries_section(args, dev, n=10_000, e=100_000, f=64, queries=8):
+    """graph_prediction with several queries: `Explainer.run_queries` (one mask
+    set per repeat shared by all queries) against the reference's usage, one `Explainer.run` per
+    query, both through the public API end to end (host orchestration included), device
+    sampler, synthetic graph, random-init 2-layer GCN + Linear head + sigmoid."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    g = torch.Generator().manual_seed(3)
+    feat = torch.randn((n, f), generator=g)
+    ei = torch.randint(0, n, (2, e), generator=g)
+    torch.manual_seed(3)
+    arch = ConvStack("gcn", [f, f, f], [f, 1]).eval()
+    params = {"seed": 1, "interpret_samples": args.interpret_samples, "epochs": args.epochs,
+              "optimizer": "adam", "lr": 0.01, "lr_patience": 10, "l1_lambda": 1e-4,
+              "mask_sampler": "device"}
+    names = [str(i) for i in range(n)]
+    exp = Explainer(feat.to(dev), ei.to(dev), arch, params, names,
+                    problem="graph_prediction")
+    els = [str(7 + 97 * i) for i in range(queries)]
+    exp.run_queries(els[:2], 1)
+    exp.run(els[0], 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    exp.run_queries(els, 1)
+    torch.cuda.synchronize()
+    t_shared = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for el in els:
+        exp.run(el, 1)
+    torch.cuda.synchronize()
+    t_loop = time.perf_counter() - t0
+    R = args.interpret_samples * args.epochs
+    return {"workload": f"graph_prediction, {n} nodes / {e} edges, {f} feats, 2-layer GCN, "
+                        f"{queries} queries x {R} rows, one repeat, device sampler",
+            "run_queries_ms": t_shared * 1e3, "run_per_query_ms": t_loop * 1e3,
+            "samples_per_s_shared": queries * R / t_shared,
+            "samples_per_s_per_query_runs": queries * R / t_loop,
+            "speedup": t_loop / t_shared}
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -625,6 +665,9 @@ def main():
                 torch.cuda.empty_cache()
             if comm is not None:
                 regimes["communities_c2"] = comm
+            if not args.no_communities:
+                regimes["graph_queries"] = graph_queries_section(args, dev)
+                torch.cuda.empty_cache()
             if regimes:
                 line["regimes"] = regimes
         print(json.dumps(line), flush=True)
