@@ -496,21 +496,22 @@ def test_device_sampler_run_is_sane():
 @pytest.mark.parametrize("sampler", ["compat", "device"])
 def test_run_queries_shares_masks(sampler):
     """Explainer.run_queries (graph_prediction, one mask set for several queries): with the
-    same seed, query 0 reproduces `run` exactly (same masks, same initial weights — the extra
-    queries' inits are drawn after it), and each further query gets its own fit."""
+    same seed, query 0 reproduces `run` (same masks, same initial weights — the extra queries'
+    inits are drawn after it; atol 1e-4, the surrogate-weight bar, since the batched fit launch
+    splits each fit over fewer workgroups), and each further query gets its own fit."""
     from case_builders import build_explainer
     exp, z, meta = build_explainer("gcn2_graph", {"mask_sampler": sampler})
     el = meta["element"]
     other = next(n for n in exp.names if str(n) != str(el))
     df_ref, pdf_ref = exp.run(el, 1)
     (df0, pdf0), (df1, pdf1) = exp.run_queries([el, other], 1)
-    np.testing.assert_allclose(df0.loc[df_ref.index].values, df_ref.values, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(df0.loc[df_ref.index].values, df_ref.values, rtol=0, atol=1e-4)
     assert list(df1.columns) == list(df_ref.columns) and len(df1) == len(df_ref)
     assert not np.isnan(df1.values).any() and not df1.equals(df0)
     if pdf_ref is not None:
-        np.testing.assert_allclose(pdf0.loc[pdf_ref.index].values, pdf_ref.values, atol=1e-6)
+        np.testing.assert_allclose(pdf0.loc[pdf_ref.index].values, pdf_ref.values, atol=1e-4)
     [(dfs, _)] = exp.run_queries([el], 1)
-    np.testing.assert_allclose(dfs.loc[df_ref.index].values, df_ref.values, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(dfs.loc[df_ref.index].values, df_ref.values, rtol=0, atol=1e-4)
 
 
 def test_device_community_sampler_run():
