@@ -313,7 +313,12 @@ class Explainer:
             set_seed(self.params["seed"])
         self.arch = self.arch.to(device).eval()
         c = self.prepare(elements[0], device)
-        inds = [c["sub_ind"]] + [self.prepare(e, device)["sub_ind"] for e in elements[1:]]
+        # graph_prediction: every query indexes the same (whole) graph, so only the element
+        # lookup of `prepare` differs per query (explainer.py:427-447)
+        inds = [c["sub_ind"]]
+        for e in elements[1:]:
+            ind = self.extract_index(e, c["sub_names"])
+            inds.append(int(ind.reshape(-1)[0]) if isinstance(ind, torch.Tensor) else ind)
         sub_feat, sub_ei, S = c["sub_feat"], c["sub_ei"], c["S"]
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
         plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, inds, *geo)
