@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -22,6 +22,11 @@ c_i32, c_i64, c_f32, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctyp
 
 class NativeLibraryError(RuntimeError):
     pass
+
+
+class FitExchangeError(RuntimeError):
+    """The multi-workgroup surrogate fit's cross-workgroup exchange timed out (its workgroups
+    were not all resident on the GPU at once): the fit's outputs are invalid."""
 
 
 class TermDesc(ctypes.Structure):
@@ -74,7 +79,7 @@ _SIGS = {
                             ctypes.c_size_t, c_vp], c_i32),
     "xpg_wlm_workspace": ([c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)], c_i32),
     "xpg_wlm_fit": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, ctypes.POINTER(WlmParams), c_i64,
-                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
+                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
     "xpg_khop_workspace": ([c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)], c_i32),
     "xpg_khop_subgraph": ([c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                            ctypes.c_size_t, c_vp], c_i32),

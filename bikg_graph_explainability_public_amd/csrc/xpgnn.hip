@@ -2501,9 +2501,11 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     const double* __restrict__ kern,
     const WlmStep* __restrict__ stp, xpg_wlm_params Pm, float* __restrict__ wg, float* __restrict__ mg,
     float* __restrict__ vg, float* __restrict__ p_hist, float* __restrict__ w_hist, uint64_t* xp,
-    uint32_t* err) {
+    uint32_t* err, uint32_t spin_limit, int fault_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int abort_s;  // set by any lane whose poll timed out (or saw the error word): leave the step loop
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) abort_s = 0;
   int64_t f;
   int part;
   if (xcd_local) {  // blocks b and b + 8 share an XCD (observed round-robin dealing, speed only)
@@ -2655,7 +2657,8 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     // row j until it carries this step's tag
     uint64_t* xs = xp + (t & 1) * P * (int64_t)batch;
     const uint32_t tag = static_cast<uint32_t>(t + 1);
-    for (int j = tid; j < B; j += 1024) {
+    const bool skip_pub = fault_part == part && f == 0 && t == 0;  // fault injection (tests only)
+    for (int j = tid; j < B && !skip_pub; j += 1024) {
       float p = 0.f;
       for (int sl = 0; sl < n_bs; ++sl) p += bpart[sl * batch + j];
       st64_sc1(xs + part * (int64_t)batch + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(p));
@@ -2686,8 +2689,14 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
               while (static_cast<uint32_t>(gr >> 32) != tag) {
                 __builtin_amdgcn_s_sleep(1);
                 gr = ld64_sc1(src);
-                if (++n > kMcSpinLimit) {
+                ++n;
+                // bounded: a partner that never publishes (grid not co-resident, or a partner
+                // that already left after an error) ends the fit with the error word set, which
+                // xpg_wlm_fit hands to the caller's status word
+                if (n > spin_limit || ((n & 63u) == 0 &&
+                                       __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                   __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  abort_s = 1;
                   break;
                 }
               }
@@ -2714,6 +2723,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     XPG_STAMP(4)
     lds_barrier();  // G and Cb(t) complete; Rb, kbuf free
     XPG_STAMP(5)
+    if (abort_s) break;  // workgroup-uniform (read after the barrier): the fit is invalid, stop
     if (t + 1 < nsteps) XPG_MC_ROWS_LOAD(t + 1)
     // ---- D: gradient of the own columns (lanes = columns)
     for (int it = wave; it < ncb * n_ds; it += 16) {
@@ -3824,6 +3834,10 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   if (rows == 0) return XPG_OK;
   {
     const char* env = getenv("XPG_FORWARD");
+    // XPG_FORWARD_STRICT=1 (tests): a forced path that does not take the plan is an error
+    // instead of a fall-back to the multi-kernel path
+    const char* strict_env = getenv("XPG_FORWARD_STRICT");
+    const bool strict = env && *env && std::strcmp(env, "unfused") != 0 && strict_env && std::strcmp(strict_env, "1") == 0;
     const bool multi = env && std::strcmp(env, "unfused") == 0;
     const bool wave_rows = env && std::strcmp(env, "fused") == 0;
     if (wave_rows) {
@@ -3833,6 +3847,7 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
       rc = try_rows_forward(p, bits, rows, y, st);
       if (rc != 1) return rc;
     }
+    if (strict) return fail(XPG_EINVAL, "masked_forward: the forced XPG_FORWARD path does not take this plan");
   }
   char* ws = static_cast<char*>(workspace);
   float* kin = reinterpret_cast<float*>(ws + L.kin);
@@ -4103,7 +4118,7 @@ int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
 int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                 const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
                 float* w, float* adam_m, float* adam_v, double* losses, int32_t* best_epoch,
-                void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
+                int32_t* status, void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
   XPG_REQ(params != nullptr, "wlm_fit: params required");
   XPG_REQ(n_fits <= 65535, "wlm_fit: at most 65535 fits per launch");
   WlmWs L;
@@ -4113,6 +4128,7 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   hipStream_t st = S(stream);
   char* ws = static_cast<char*>(workspace);
   WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
+  if (status) XPG_HIP(hipMemsetAsync(status, 0, sizeof(int32_t), st));
   if (L.grid) return wlm_fit_grid(n_fits, bits, rows, cols, batch, y, kernel, *params, step0, w, adam_m, adam_v,
                                   losses, best_epoch, ws, L, st);
   uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
@@ -4138,6 +4154,11 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
     XPG_HIP(hipMemsetAsync(xp, 0, sizeof(uint64_t) * 2 * L.P * (size_t)batch * n_fits, st));
     XPG_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n_fits + 1), st));
     const int cpt_mc = static_cast<int>(cdiv((int64_t)L.wpp * 32, 1024));
+    // test hooks: XPG_MC_SPIN (poll bound), XPG_MC_FAULT (part of fit 0 that skips its first publish)
+    const char* se = getenv("XPG_MC_SPIN");
+    const char* fe = getenv("XPG_MC_FAULT");
+    const uint32_t spin = se ? static_cast<uint32_t>(strtoul(se, nullptr, 10)) : kMcSpinLimit;
+    const int fault = fe ? atoi(fe) : -1;
     const dim3 grid(static_cast<unsigned>(L.xcd ? 8 * L.P * cdiv(n_fits, 8) : n_fits * L.P));
 #define XPG_WLM_MC(C)                                                                                       \
     if (!launched && cpt_mc <= C) {                                                                         \
@@ -4145,13 +4166,15 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_mc))); \
       hipLaunchKernelGGL(k_wlm_fit_mc<C>, grid, dim3(1024), L.lds_mc, st, bits, colbits, rows, ic, words, ib, L.bw, \
                          L.P, L.wpp, L.mc_bs, L.mc_ds, n_fits, L.xcd ? 1 : 0, kernel, stp, *params, w, adam_m,    \
-                         adam_v, p_hist, w_hist, xp, cnt + n_fits);                                         \
+                         adam_v, p_hist, w_hist, xp, cnt + n_fits, spin, fault);                           \
       XPG_LAUNCHED();                                                                                       \
       launched = true;                                                                                      \
     }
     XPG_WLM_MC(1) XPG_WLM_MC(2) XPG_WLM_MC(4)
 #undef XPG_WLM_MC
     if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported slice width");
+    // the exchange's error word (nonzero: a partner's poll timed out, the weights are invalid)
+    if (status) XPG_HIP(hipMemcpyAsync(status, cnt + n_fits, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
   }
   const int cpt = static_cast<int>(cdiv(cols, 1024));
 #define XPG_WLM(C, TL)                                                                                     \

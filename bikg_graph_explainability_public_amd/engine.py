@@ -422,11 +422,26 @@ def _workspace(dev, nbytes):
     return t
 
 
-def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0):
+def check_fit_status(status):
+    """Raise FitExchangeError when a fit's device status word (see wlm_fit) is nonzero.  Reads
+    the word, i.e. waits for the stream to reach the end of that fit."""
+    if int(status.max().item()) != 0:
+        raise _lib.FitExchangeError(
+            "surrogate fit: the multi-workgroup exchange timed out (workgroups not co-resident, "
+            "e.g. another kernel or process held the GPU's CUs); the fitted weights are invalid. "
+            "XPG_WLM=single selects the single-workgroup fit.")
+
+
+def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0, check=True,
+            status=None):
     """train_model (wlm.py:132-278) epoch loop on device for one or many independent fits.
 
     bits [R, W] or [F, R, W]; y / kernel [R] or [F, R]; w0 [S] or [F, S].  Returns
-    (w, losses, best_epoch, adam_m, adam_v) with the same leading fit dimension (if any)."""
+    (w, losses, best_epoch, adam_m, adam_v) with the same leading fit dimension (if any).
+
+    check=True reads the fit's status word and raises FitExchangeError if the multi-workgroup
+    exchange failed (one stream sync).  check=False leaves that to the caller: pass `status`
+    (device int32 [1]) and call check_fit_status(status) later (e.g. after a timed region)."""
     dev = bits.device
     batched = bits.dim() == 3
     F = bits.shape[0] if batched else 1
@@ -450,9 +465,13 @@ def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0)
     n = ctypes.c_size_t(0)
     _lib.check(_lib.load().xpg_wlm_workspace(F, rows, cols, batch, ctypes.byref(n)))
     ws = _workspace(dev, n.value)
+    if status is None:
+        status = torch.empty(1, dtype=torch.int32, device=dev)
     call("xpg_wlm_fit", F, ptr(bb), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
-         int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(ws), ws.numel(),
-         _lib.stream_of(dev))
+         int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(status), ptr(ws),
+         ws.numel(), _lib.stream_of(dev))
+    if check:
+        check_fit_status(status)
     if not batched:
         return w[0], losses[0], best[0:1], m[0], v[0]
     return w, losses, best, m, v

@@ -183,6 +183,9 @@ class Explainer:
         device = torch.device("cuda", torch.cuda.current_device())
         if times == 1:
             set_seed(self.params["seed"])
+        # multi-GPU: every rank continues from rank 0's generator, so all ranks draw the same
+        # masks / sampler seeds / initial weights (checked by checksum below)
+        sharding.sync_rng(self.group)
         self.arch = self.arch.to(device).eval()
         c = self.prepare(element, device)
         sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
@@ -236,6 +239,8 @@ class Explainer:
         # every rank returns the single-GPU result (sharding.py).
         flat = bits.reshape(times * R, -1)
         g = self.group
+        sharding.assert_replicated(bits, "mask rows", g)
+        sharding.assert_replicated(torch.stack(w0_list), "initial surrogate weights", g)
         # multi-node-type graphs: the reference's per-copy loop zeroes copies without edges and
         # its extraction re-cuts the [B] outputs (quirk Q4); params["hetero_q4"] = False keeps
         # the per-copy outputs instead (model.py:118-253, wlm.py:435-436)
@@ -279,7 +284,8 @@ class Explainer:
         best = sharding.gather_rows(fits["best"], times, g)
         config_vals = [w[i] for i in range(times)]
         diag = [{"losses": losses[i], "best_epoch": best[i], "rows": R, "batch": batch,
-                 "y": y[i], "bits": bits[i]} for i in range(times)]
+                 "y": y[i], "bits": bits[i], "kernel": kern[i], "w0": w0_list[i]}
+                for i in range(times)]
         mean, std = self.weight_stacking(config_vals)
         config_val_df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
         pathway_df = None
@@ -297,11 +303,15 @@ class Explainer:
         each time.  In graph_prediction every query perturbs the same S = N columns
         (explainer.py:427-447), so here each repeat's masks are drawn once, one masked forward
         produces every query's logit per row (a multi-query ForwardPlan), KernelSHAP runs once,
-        and each query gets its own surrogate fits (all of them in one launch).  RNG order per repeat: masks, then one
-        LinearRegression init per query, then the DataLoader seed draw — with one query this is
-        exactly `run`'s order, so `run_queries([e]) == [run(e)]` (to the fit's 1e-4 bar when the
-        batched launch splits each fit over fewer workgroups).  Returns [(config_val_df,
-        pathway_df)] in `elements` order.  Engine-compilable single-node-type archs only."""
+        and each query gets its own surrogate fits (all of them in one launch while the
+        replicated mask rows stay under params["run_queries_batch_bytes"], default 2 GiB; else
+        one launch per query).  RNG order per repeat: masks, then one LinearRegression init per
+        query, then the DataLoader seed draw — with one query this is exactly `run`'s order, so
+        `run_queries([e]) == [run(e)]` (to the fit's 1e-4 bar when the batched launch splits each
+        fit over fewer workgroups).  Multi-GPU: like `run`, the rows of the forward / KernelSHAP
+        are sharded over ranks with one all-gather each, and the Q x times fits are sharded over
+        ranks.  Returns [(config_val_df, pathway_df)] in `elements` order.  Engine-compilable
+        single-node-type archs only."""
         assert "graph" in self.problem, \
             "run_queries shares one mask set across queries: graph_prediction problems only"
         if not torch.cuda.is_available():
@@ -311,6 +321,8 @@ class Explainer:
         device = torch.device("cuda", torch.cuda.current_device())
         if times == 1:
             set_seed(self.params["seed"])
+        g = self.group
+        sharding.sync_rng(g)
         self.arch = self.arch.to(device).eval()
         c = self.prepare(elements[0], device)
         # graph_prediction: every query indexes the same (whole) graph, so only the element
@@ -321,14 +333,14 @@ class Explainer:
             inds.append(int(ind.reshape(-1)[0]) if isinstance(ind, torch.Tensor) else ind)
         sub_feat, sub_ei, S = c["sub_feat"], c["sub_ei"], c["S"]
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
+        Q = len(inds)
+        assert len(set(inds)) == Q, "run_queries: duplicate query elements"
         plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, inds, *geo)
         assert plan is not None and not getattr(plan, "multi_type", False), \
             "run_queries needs an engine-compilable single-node-type architecture"
         if self.params.get("verify_arch", True):
-            ok, err = pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, inds[0], *geo)
+            ok, err = pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, inds, *geo)
             assert ok, f"compiled arch disagrees with its torch forward (max err {err:.3g})"
-        Q = len(inds)
-        assert len(set(inds)) == Q, "run_queries: duplicate query elements"
         sampler = self.params.get("mask_sampler", "compat")
         _, epochs = Mask.assertions_mask_generator(self.params)
         if sampler == "device" and c["sub_pw_inds"] is not None:
@@ -354,21 +366,39 @@ class Explainer:
         R = bits_list[0].shape[0]
         batch = R // epochs
         bits = torch.stack(bits_list)                       # [times, R, W]
+        w0_all = torch.stack([w for wq in w0 for w in wq])  # [Q * times, S], query-major
+        sharding.assert_replicated(bits, "mask rows", g)
+        sharding.assert_replicated(w0_all, "initial surrogate weights", g)
         flat = bits.reshape(times * R, -1)
-        y = plan.forward(flat).reshape(times, R, -1)        # [times, R, >= Q]
-        kern = engine.shap_kernel(flat, S).reshape(times, R)
-        # all Q x times fits in one launch (independent fits run concurrently; each is a chain
-        # of sequential Adam steps) while the replicated mask rows stay small; else per query
-        if Q * bits.numel() * 4 <= (2 << 30):
-            ws, _, _, _, _ = engine.wlm_fit(
-                bits.unsqueeze(0).expand(Q, -1, -1, -1).reshape(Q * times, R, -1), S, batch,
-                y[:, :, :Q].permute(2, 0, 1).reshape(Q * times, R),
-                kern.unsqueeze(0).expand(Q, -1, -1).reshape(Q * times, R),
-                torch.stack([w for wq in w0 for w in wq]), self.params)
-            fitted = [ws[q * times:(q + 1) * times] for q in range(Q)]
-        else:
-            fitted = [engine.wlm_fit(bits, S, batch, y[:, :, q].contiguous(), kern,
-                                     torch.stack(w0[q]), self.params)[0] for q in range(Q)]
+        y = sharding.gather_map(times * R, lambda s, e: plan.forward(flat[s:e])[:, :Q],
+                                g).reshape(times, R, Q)
+
+        def kernel_rows(s, e):
+            if e == s:
+                return torch.empty(0, dtype=torch.float64, device=device)
+            return engine.shap_kernel(flat[s:e], S)
+        kern = sharding.gather_map(times * R, kernel_rows, g).reshape(times, R)
+        limit = int(self.params.get("run_queries_batch_bytes", 2 << 30))
+
+        def fit(u0, u1):
+            # units u = q * times + i (query q, repeat i), a contiguous shard of them
+            if u1 == u0:
+                return torch.empty((0, S), device=device)
+            us = torch.arange(u0, u1, device=device)
+            q_of, i_of = us // times, us % times
+            if (u1 - u0) * bits[0].numel() * 4 <= limit:
+                ws, _, _, _, _ = engine.wlm_fit(
+                    bits[i_of], S, batch, y[i_of, :, q_of], kern[i_of], w0_all[u0:u1],
+                    self.params)
+                return ws
+            out = []  # one launch per query (its repeats batched)
+            for q in range(int(q_of[0]), int(q_of[-1]) + 1):
+                sel = (q_of == q).nonzero().reshape(-1)
+                ii = i_of[sel]
+                out.append(engine.wlm_fit(bits[ii], S, batch, y[ii, :, q], kern[ii],
+                                          w0_all[(u0 + sel).cpu()], self.params)[0])
+            return torch.cat(out)
+        fitted = sharding.gather_map(Q * times, fit, g).reshape(Q, times, S)
         out = []
         for q in range(Q):
             w = fitted[q]
@@ -378,6 +408,9 @@ class Explainer:
             if c["has_pathways"]:
                 pdf = Pathways(c["sub_pw"], c["sub_pw_names"]).aggregate(mean, c["sub_pw_inds"])
             out.append((df, pdf))
+        self.last_run = {"engine": True, "queries": inds, "S": S, "rows": R, "batch": batch,
+                         "bits": bits, "y": y, "kernel": kern, "w0": w0_all.reshape(Q, times, S),
+                         "weights": fitted, "plan": plan}
         return out
 
 

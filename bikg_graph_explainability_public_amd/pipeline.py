@@ -110,7 +110,12 @@ def generic_outputs(arch, feat, edge_index, mask, element_index, problem, node_t
                     padded_dims=None, batch=None, q4=True):
     """wlm.py:349-436 semantics per batch of mask rows with the user's module in torch.
     Returns y [R] (the regression target of each row; for multi-node-type graphs the
-    reference's output[ind::S] collapse, quirk Q4, broadcast over its batch)."""
+    reference's output[ind::S] collapse, quirk Q4, broadcast over its batch).  A list of
+    element indices (single-node-type graphs) returns y [R, Q]: every query's extraction from
+    the same union-graph forward."""
+    if isinstance(element_index, (list, tuple)):
+        return _generic_multi(arch, feat, edge_index, mask, element_index, problem, node_type,
+                              edge_type, node_type_names, edge_type_names, padded_dims, batch)
     data = Data(feat, edge_index)
     mc = Model(arch)
     R, S = mask.shape
@@ -155,15 +160,48 @@ def generic_outputs(arch, feat, edge_index, mask, element_index, problem, node_t
     return torch.cat(ys)
 
 
+def _generic_multi(arch, feat, edge_index, mask, queries, problem, node_type, edge_type,
+                   node_type_names, edge_type_names, padded_dims, batch):
+    """generic_outputs for several queries of a single-node-type graph: [R, Q]."""
+    data = Data(feat, edge_index)
+    mc = Model(arch)
+    R, S = mask.shape
+    batch = R if batch is None else batch
+    ys = []
+    for r0 in range(0, R, batch):
+        mb = mask[r0:r0 + batch]
+        B = mb.shape[0]
+        cf, cnt, pei, pet = data.perturbator(mb, problem, node_type, edge_type)
+        pei = pei.long()
+        if node_type is not None and edge_type is not None and node_type_names is not None \
+                and edge_type_names is not None:
+            cf = data.homo2hetero(cf, cnt, node_type_names, padded_dims)
+            pei = data.homo2hetero(pei, pet, edge_type_names)
+        out = mc.infer(cf, pei, cnt, pet)
+        if isinstance(out, dict):
+            out, _ = mc.hetero2homo_output(out)
+        ys.append(torch.stack([mc.extract_node_edge_output(out, int(q), S).reshape(-1).float()
+                               for q in queries], 1).reshape(B, len(queries)))
+    return torch.cat(ys)
+
+
 def verify_plan(plan, arch, feat, edge_index, query, node_type=None, edge_type=None,
                 node_type_names=None, edge_type_names=None, padded_dims=None, rows=8, tol=1e-4):
     """Check the compiled program against the user's module on a few random masks (guards the
-    registration-order lowering in program.compile_arch)."""
+    registration-order lowering in program.compile_arch).  `query` may be the list of a
+    multi-query plan's queries: every output column is then checked."""
     g = torch.Generator(device="cpu").manual_seed(1234)
     S = feat.shape[0]
     mask = (torch.rand((rows, S), generator=g) < 0.5).to(feat.device)
     mask[0] = True
     multi = getattr(plan, "multi_type", False)
+    if isinstance(query, (list, tuple)):
+        assert not multi, "multi-query plans are single-node-type"
+        ref = generic_outputs(arch, feat, edge_index, mask, list(query), "node", node_type,
+                              edge_type, node_type_names, edge_type_names, padded_dims)
+        got = plan.forward(engine.pack_masks(mask))[:, :len(query)]
+        err = (ref - got).abs().max().item()
+        return err <= tol * max(1.0, ref.abs().max().item()), err
     ref = generic_outputs(arch, feat, edge_index, mask, query, "node", node_type, edge_type,
                           node_type_names, edge_type_names, padded_dims, q4=not multi)
     bits = engine.pack_masks(mask)

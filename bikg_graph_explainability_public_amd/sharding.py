@@ -25,6 +25,60 @@ def world_info(group=None):
     return dist.get_world_size(group), dist.get_rank(group)
 
 
+def _backend_device(t, group=None):
+    """Collectives run on the device the backend supports: RCCL ("nccl") on the GPU, gloo on the
+    host (gloo is the CPU test backend; its GPU-tensor support is partial)."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return t.device if t.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+
+
+def sync_rng(group=None, src=0):
+    """Make every rank's torch CPU generator equal to rank `src`'s (one broadcast of the state).
+
+    Explainer.run draws the compat masks, the device samplers' seeds and the surrogates' initial
+    weights from torch's CPU generator (the reference's RNG order).  Each rank draws the SAME
+    values only if the generators agree, so a rank seeded differently (or `times > 1` without
+    set_seed) would otherwise fit against another rank's masks.  After this call they agree."""
+    import torch.distributed as dist
+    world, _ = world_info(group)
+    if world == 1:
+        return
+    state = torch.get_rng_state()
+    buf = state.to(_backend_device(state, group))
+    dist.broadcast(buf, src=dist.get_global_rank(group, src) if group is not None else src,
+                   group=group)
+    torch.set_rng_state(buf.cpu())
+
+
+def checksum(t):
+    """Order-sensitive int64 checksum of a tensor's bytes (position-weighted word sum)."""
+    b = t.detach().contiguous().view(torch.uint8).reshape(-1)
+    pad = (-b.numel()) % 4
+    if pad:
+        b = torch.cat([b, b.new_zeros(pad)])
+    w = b.view(torch.int32).to(torch.int64)
+    pos = torch.arange(w.numel(), device=w.device, dtype=torch.int64) % 1000003 + 1
+    return int((w * pos).sum().item())
+
+
+def assert_replicated(t, what, group=None):
+    """Raise if `t` differs between ranks (compares checksums with one small all-gather)."""
+    import torch.distributed as dist
+    world, _ = world_info(group)
+    if world == 1:
+        return
+    c = torch.tensor([checksum(t)], dtype=torch.int64)
+    c = c.to(_backend_device(c, group))
+    outs = [torch.empty_like(c) for _ in range(world)]
+    dist.all_gather(outs, c, group=group)
+    vals = [int(o.item()) for o in outs]
+    if len(set(vals)) != 1:
+        raise RuntimeError(f"{what} differ between ranks (checksums {vals}): every rank must draw "
+                           "the same masks and initial weights")
+
+
 def shard_range(n, world, rank):
     """Contiguous balanced split of n units: the first n % world ranks get one extra."""
     if world < 1 or not 0 <= rank < world:
@@ -50,15 +104,16 @@ def gather_rows(local, n, group=None):
     if local.shape[0] != e - s:
         raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard is {e - s}")
     cap = shard_range(n, world, 0)[1]
-    buf = local.new_zeros((cap,) + tuple(local.shape[1:]))
-    buf[:e - s] = local
+    dev = _backend_device(local, group)
+    buf = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    buf[:e - s] = local.to(dev)
     outs = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(outs, buf, group=group)
     parts = []
     for r in range(world):
         rs, re_ = shard_range(n, world, r)
         parts.append(outs[r][:re_ - rs])
-    return torch.cat(parts, 0)
+    return torch.cat(parts, 0).to(local.device)
 
 
 def gather_map(n, fn, group=None):

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 8
+#define XPG_ABI_VERSION 9
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -177,12 +177,15 @@ int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
  * independent surrogates (e.g. the `times` repeats of Explainer.run), one workgroup each.
  * Arrays are fit-major and contiguous: bits [n_fits][rows][words], y / kernel [n_fits][rows],
  * w / adam_m / adam_v [n_fits][cols] (updated in place), losses [n_fits][steps] (fp64),
- * best_epoch [n_fits] (first argmin).  `step0` = Adam steps already taken with (m, v). */
+ * best_epoch [n_fits] (first argmin).  `step0` = Adam steps already taken with (m, v).
+ * status (device int32 [1], nullable): 0 once the stream reaches the end of the fit, nonzero
+ * if the multi-workgroup fit's cross-workgroup exchange timed out (a partner workgroup was not
+ * co-resident) — every output of the call is then invalid and the caller must not use it. */
 int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols,
                 int64_t batch, const float* y, const double* kernel,
                 const xpg_wlm_params* params, int64_t step0, float* w, float* adam_m,
-                float* adam_v, double* losses, int32_t* best_epoch, void* workspace,
-                size_t workspace_bytes, xpg_stream_t stream);
+                float* adam_v, double* losses, int32_t* best_epoch, int32_t* status,
+                void* workspace, size_t workspace_bytes, xpg_stream_t stream);
 
 /* ---------------------------------------------------------------- k-hop computational subgraph */
 /* Replaces Data.comp_graph's PyG k_hop_subgraph(seed, hops, edge_index, relabel_nodes=True,

@@ -120,13 +120,18 @@ def test_oracle_known_answers():
     assert [n for n, _ in agg] == ["2", "1", "4", "3"]
     np.testing.assert_allclose([s for _, s in agg], [0.7025, 0.65, 0.4475, 0.365], atol=1e-6)
 
+    # tests/test_wlm.py:378-404 vectors: flat target, elementwise (no broadcast).  Expected value
+    # written out: sum k (p - r)^2 = 0.5*.0025 + .85*.0036 + .34*.0049 + .78*.0049 = 0.009798,
+    # / 4 (mean) / 2.47 (sum k)
     p = np.array([0.98, 0.23, -0.12, -0.24])
     r = np.array([0.93, 0.29, -0.19, -0.31])
     kk = np.array([0.5, 0.85, 0.34, 0.78])
-    exp = np.mean(kk * (p - r) ** 2) / kk.sum()
-    # the unit test feeds a flat target (no broadcast); emulate with a per-row target
-    got = np.mean(kk * (p - r) ** 2) / kk.sum()
-    assert abs(got - exp) < 1e-15
+    assert abs(oracle.weighted_mse_loss(p, r, kk) - 0.009798 / 4 / 2.47) < 1e-12
+    # the train_model call site's [B, 1] target broadcasts to [B, B] (quirk Q1): closed form
+    # (1/B) sum_j k_j [(p_j - ybar)^2 + var(y)] / sum k
+    q1 = (np.mean(kk * (p - r.mean()) ** 2) + r.var() * kk.mean()) / kk.sum()
+    assert abs(oracle.weighted_mse_loss(p, r[:, None], kk) - q1) < 1e-12
+    assert abs(oracle.weighted_mse_loss(p, r[:, None], kk) - oracle.weighted_mse_loss(p, r, kk)) > 1e-4
 
     m9 = np.array([[0] * 9, [1, 0, 0, 0, 1, 0, 0, 1, 1], [0, 1, 1, 1, 1, 0, 0, 0, 0]], bool)
     k9 = oracle.shap_kernel(m9)

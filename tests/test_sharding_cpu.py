@@ -91,6 +91,56 @@ def _worker_pipeline(rank, world, port):
         dist.destroy_process_group()
 
 
+def _draw_repeat():
+    """One repeat's RNG-dependent draws in Explainer.run's order (compat host sampler on the
+    test_run fixture with its 4 communities, then the surrogate's initial weights)."""
+    from bikg_graph_explainability_public_amd.masks import Mask, dataloader_seed_draw
+    from bikg_graph_explainability_public_amd.wlm import LinearRegression
+    from golden_utils import load_case
+    z, meta = load_case("test_run")
+    S = 15
+    pathways = [[0, 1, 2, 3], [4, 5, 6], [7, 8, 9, 10, 11], [12, 13, 14, 2]]
+    mask, _ = Mask(torch.zeros((S, 4)), torch.zeros((2, 0), dtype=torch.long), pathways,
+                   meta["params"], "node_prediction").generate()
+    w0 = LinearRegression(S).layer.weight.detach().reshape(-1).clone()
+    dataloader_seed_draw()
+    return mask, w0
+
+
+def _worker_rng(rank, world, port, ref_path):
+    _init(rank, world, port)
+    try:
+        torch.manual_seed(500 + 31 * rank)            # ranks seeded differently
+        try:                                          # unsynchronised draws differ between ranks
+            sharding.assert_replicated(_draw_repeat()[0], "mask rows")
+        except RuntimeError:
+            pass
+        else:
+            raise AssertionError("differently seeded ranks were not detected")
+        torch.manual_seed(500 + 31 * rank)
+        sharding.sync_rng()                           # rank 0's generator everywhere
+        mask, w0 = _draw_repeat()
+        sharding.assert_replicated(mask, "mask rows")
+        sharding.assert_replicated(w0, "initial weights")
+        ref = torch.load(ref_path, weights_only=True)
+        assert torch.equal(mask, ref["mask"]) and torch.equal(w0, ref["w0"])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sync_rng_ranks_seeded_differently_gloo(world, tmp_path):
+    """Explainer.run's multi-rank RNG contract (sharding.sync_rng + assert_replicated): ranks
+    seeded differently draw different masks (detected by the checksum all-gather); after
+    sync_rng every rank draws the masks and initial weights of a single process seeded like
+    rank 0 (the reference's RNG order: mask_generator, LinearRegression init, DataLoader seed)."""
+    torch.manual_seed(500)
+    mask, w0 = _draw_repeat()
+    ref_path = str(tmp_path / "ref.pt")
+    torch.save({"mask": mask, "w0": w0}, ref_path)
+    mp.spawn(_worker_rng, args=(world, _free_port(), ref_path), nprocs=world, join=True)
+
+
 def test_shard_range_partitions():
     for n in (0, 1, 5, 12800, 12801):
         for world in (1, 2, 3, 8):

@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
     hipMemcpy(d_m, z.data(), S * 4, hipMemcpyHostToDevice);
     hipMemcpy(d_v, z.data(), S * 4, hipMemcpyHostToDevice);
     hipEventRecord(a, 0);
-    int rc = xpg_wlm_fit(1, d_bits, R, S, batch, d_y, d_k, &P, 0, d_w, d_m, d_v, d_l, d_b, ws, wsb, 0);
+    int rc = xpg_wlm_fit(1, d_bits, R, S, batch, d_y, d_k, &P, 0, d_w, d_m, d_v, d_l, d_b, nullptr, ws, wsb, 0);
     hipEventRecord(b, 0);
     hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
