@@ -1,23 +1,36 @@
 """Benchmark: perturbation-samples/s of the XP-GNN hot path on MI355X (BASELINE.json metric).
 
-Workload (configs[1] of BASELINE.json, "c2"): synthetic homogeneous graph, 100k nodes / 1M
-edges, 64-dim fp32 features, 2-layer GCN 64->64->64 + Linear(64->1) + sigmoid (random init),
+Headline (`value`), configs[1] ("c2"): synthetic homogeneous graph, 100k nodes / 1M edges,
+64-dim fp32 features, 2-layer GCN 64->64->64 + Linear(64->1) + sigmoid (random init),
 interpret_samples=256, epochs=50 -> 12,800 mask rows per repeat, query node 7 (node_prediction:
 its 3-hop computational subgraph, as the reference extracts it).
 
-One step = one full repeat of the hot path per rank, inputs resident in HBM:
-  device mask sampling (Philox Shapley rows) -> masked receptive-field forward (all rows) ->
-  KernelSHAP weights -> surrogate Adam loop (ceil(R / (R // epochs)) steps) ->
-  (N > 1) all-gather of the per-repeat weights for the mean/std over repeats.
-Repeats are independent, so ranks shard repeats (weak scaling, one repeat per rank per step).
+One step = one repeat per rank through the north-star split of Explainer.run (explainer.py:490-532,
+SURVEY.md §8e), inputs resident in HBM:
+  device mask sampling (Philox Shapley rows of this rank's row shard, keyed by global row) ->
+  masked receptive-field forward of the shard -> KernelSHAP of the shard ->
+  RCCL all-gather of the per-row fp32 logits and fp64 kernel weights ->
+  surrogate Adam loops of this rank's repeats (ceil(R / (R // epochs)) steps each) ->
+  all-gather of the fitted weights -> mean / std over repeats (weight_stacking).
+With N ranks a step covers N repeats (weak scaling: one repeat's rows and one fit per rank).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+`regimes` (every N unless noted):
+  c3_full_graph   configs[2]: 1M nodes / 10M edges, 2-layer SAGE 128, 512 mask rows sharded over
+                  the ranks (strong scaling), every node a target (SURVEY.md §8d regime (ii): the
+                  >= 40 % HBM roofline target), + the all-gather of the rows' query logits
+  c5_hetero       configs[4]: 1M-node 3-type graph, 256-dim features, 20 communities, device
+                  community sampler, interpret_samples=1024, repeats=10, community scoring
+  graph_prediction_c3, hetero_c4, communities_c2, graph_queries   (N = 1 only)
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--sections a,b] [--no-cpu-baseline]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import json
 import math
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -28,7 +41,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "perturbation-samples/sec (masked GNN fwd) per query node; 1/2/4/8 GPU"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TF = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+SECTIONS = ("headline", "c3", "c5", "gp", "c4", "comm", "queries")
+MULTI_GPU_SECTIONS = ("headline", "c3", "c5")
 
 
 def parse():
@@ -43,20 +59,22 @@ def parse():
     p.add_argument("--epochs", type=int, default=50)
     p.add_argument("--query", type=int, default=7)
     p.add_argument("--repeats", type=int, default=1,
-                   help="Explainer.run(times=...) repeats per rank per step (batched fits)")
+                   help="repeats per rank per step (Explainer.run(times=...) / world)")
+    p.add_argument("--sections", default="all",
+                   help="comma list of " + ",".join(SECTIONS) + " (PMC passes run one each)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-rows", type=int, default=12800)
-    p.add_argument("--full-graph-rows", type=int, default=64,
-                   help="regime (ii): mask rows of the c3-shaped full-graph forward (0 = skip)")
-    p.add_argument("--no-hetero", action="store_true", help="skip the c4 multi-type section")
-    p.add_argument("--no-communities", action="store_true",
-                   help="skip the c2 community-sampler section")
-    p.add_argument("--no-graph-prediction", action="store_true",
-                   help="skip the c3 graph_prediction per-query pipeline section")
+    p.add_argument("--cpu-procs", type=int, default=0,
+                   help="CPU baseline worker processes (0: min(16, host cores))")
+    p.add_argument("--c3-rows", type=int, default=512,
+                   help="regime (ii): mask rows of the c3 full-graph forward (all ranks)")
+    p.add_argument("--c5-times", type=int, default=10)
+    p.add_argument("--c5-samples", type=int, default=1024)
     return p.parse_args()
 
 
-def setup_dist(args):
+# ----------------------------------------------------------------------------- plumbing
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -69,7 +87,94 @@ def setup_dist(args):
     return world, rank, local
 
 
-def build_workload(args, dev):
+def barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def log(rank, msg):
+    """Progress on stderr (rank 0): the JSON line stays the only stdout output."""
+    if rank == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def host_info():
+    model = platform.processor() or "?"
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:  # pragma: no cover
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_procs(args):
+    return args.cpu_procs or max(1, min(16, os.cpu_count() or 1))
+
+
+def _pool(n):
+    import multiprocessing as mp
+    return mp.get_context("spawn").Pool(n)
+
+
+def pmc_chain(section, kernels, ops):
+    """Counter-measured HBM bytes of ONE operation of a section's launch chain, from the
+    section's own rocprofv3 PMC passes (profiles/pmc_<section>.json, tools/pmc_traffic.py:
+    2 x FETCH_SIZE + WRITE_SIZE per dispatch, MI355X_MICROARCH.md HBM section).  `kernels` are
+    exact kernel names (template arguments stripped, no prefix matching); the file's bytes of
+    those kernels over all their dispatches are divided by `ops`, the number of operations
+    the section runs.  Returns (bytes per op, {kernel: bytes per op}) or (None, None)."""
+    fn = os.path.join(ROOT, "profiles", f"pmc_{section}.json")
+    if not os.path.exists(fn):
+        return None, None
+    data = json.load(open(fn))
+    per = {}
+    for name, d in data.items():
+        base = name.split("<")[0]
+        if base in kernels and d.get("traffic_bytes") is not None:
+            per[base] = per.get(base, 0.0) + d["traffic_bytes"] * d["dispatches"] / ops
+    if set(per) != set(kernels):
+        return None, None
+    return sum(per.values()), per
+
+
+def roofline(alg_bytes, seconds, section=None, kernels=(), ops=1, alg_per_kernel=None):
+    """The roofline object of one launch chain: algorithmic bytes per op over the measured time,
+    plus the counter-measured bytes (traffic) of the same op when the section's PMC file exists."""
+    achieved = alg_bytes / seconds / 1e9
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": alg_bytes, "traffic": None}
+    if section is not None:
+        traffic, per = pmc_chain(section, set(kernels), ops)
+        if traffic is not None:
+            out["traffic"] = traffic
+            out["traffic_source"] = f"profiles/pmc_{section}.json"
+            out["achieved_counter"] = traffic / seconds / 1e9
+            out["frac_counter"] = traffic / seconds / 1e9 / HBM_PEAK_GBS
+            out["counter_over_alg"] = traffic / alg_bytes
+            out["per_kernel_counter_bytes"] = per
+            if alg_per_kernel:
+                out["per_kernel_counter_over_alg"] = {
+                    k: per[k] / v for k, v in alg_per_kernel.items() if k in per and v}
+    return out
+
+
+# ----------------------------------------------------------------------------- c2 (headline)
+def build_c2(args, dev):
     from bikg_graph_explainability_public_amd import pipeline
     from bikg_graph_explainability_public_amd.data import Data
     from bikg_graph_explainability_public_amd.nn import ConvStack
@@ -87,72 +192,130 @@ def build_workload(args, dev):
     return arch, sub_feat, sub_ei, q, plan
 
 
-def forward_bytes(plan, rows):
-    """Algorithmic HBM bytes of the masked forward per launch chain: per row,
-    per layer: CSR pointers + columns of the targets, the row's mask words, the gathered
-    source rows of kept edges + self rows (F_out wide, layer-1 tables), the written outputs."""
-    arr = plan.arrays
-    W = (plan.cols + 31) // 32
-    b = 4 * (plan.n0 + 1) + 4 * arr["deg_src"].size + 4 * W  # degree pass
-    for li, conv in enumerate(plan.program.convs):
-        lay = arr["layers"][li]
-        n_t = arr["frontiers"][li + 1].size
-        e = lay["agg_src"].size
-        width = conv.f_out if li == 0 else conv.f_in
-        b += 4 * (n_t + 1) + 8 * e + 4 * width * (0.25 * e + n_t) + 4 * conv.f_out * n_t
-    return b * rows
-
-
 def wlm_bytes(rows, cols, batch):
+    """Algorithmic bytes of one surrogate fit: the mask bits once, y + kernel, the Adam state
+    (w, m, v read + written), one loss per step."""
     W = (cols + 31) // 32
     return rows * W * 4 + rows * (4 + 8) + cols * 4 * 6 + 8 * math.ceil(rows / batch)
 
 
-def pmc_traffic(kernels, args):
-    """HBM bytes per launch of the dominant launch chain from the committed PMC passes
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE /
-    WRITE_SIZE runs of this bench at its default configuration), or None."""
-    fn = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    default = (args.nodes, args.edges, args.feat, args.interpret_samples, args.epochs,
-               args.repeats) == (100_000, 1_000_000, 64, 256, 50, 1)
-    if not default or not os.path.exists(fn):
-        return None, None
-    data = json.load(open(fn))
-    tot, hit = 0.0, False
-    for name, d in data.items():
-        if name.startswith(kernels) and d.get("traffic_bytes") is not None:
-            tot += d["traffic_bytes"]
-            hit = True
-    return (tot if hit else None), ("profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE, "
-                                    "summed over the chain's kernels)" if hit else None)
+WLM_KERNELS = ("k_wlm_stats", "k_wlm_colbits", "k_wlm_fit_mc", "k_wlm_loss", "k_argmin_first")
 
 
-def pmc_traffic_counts(counts):
-    """HBM bytes of one operation = sum over kernels of (dispatches per operation) x (measured
-    bytes per dispatch) from profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE of this bench's
-    default run, tools/pmc_traffic.py), or None when a kernel is missing."""
-    fn = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(fn):
-        return None
-    data = json.load(open(fn))
-    tot = 0.0
-    for prefix, n in counts.items():
-        hits = [d["traffic_bytes"] for name, d in data.items()
-                if name.startswith(prefix) and d.get("traffic_bytes") is not None]
-        if not hits:
-            return None
-        tot += n * sum(hits) / len(hits)
-    return tot
+def headline(args, dev, world, rank):
+    """The c2 repeat pipeline, sharded as Explainer.run shards it (module docstring)."""
+    from bikg_graph_explainability_public_amd import engine, sharding
+    arch, sub_feat, sub_ei, q, plan = build_c2(args, dev)
+    S = plan.cols
+    R = args.interpret_samples * args.epochs
+    batch = R // args.epochs
+    times = args.repeats * world
+    n_rows = times * R
+    r0, r1 = sharding.shard_range(n_rows, world, rank)
+    f0, f1 = sharding.shard_range(times, world, rank)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    stream = torch.cuda.current_stream()
+    w0 = torch.zeros((times, S), device=dev)
+    statuses = []
+    phases = ("sample", "forward", "shap", "gather", "wlm")
+    ev = {k: [] for k in phases}
+
+    def step(i, record):
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
+        mk = (lambda j: marks[j].record(stream)) if record else (lambda j: None)
+        seed = 1000 + i
+        mk(0)
+        bits = engine.sample_shapley(seed, r1 - r0, S, dev, row_offset=r0)
+        mk(1)
+        y_loc = plan.forward(bits)[:, 0]
+        mk(2)
+        k_loc = engine.shap_kernel(bits, S)
+        mk(3)
+        y = sharding.gather_rows(y_loc, n_rows)           # RCCL all-gather of the logits
+        k = sharding.gather_rows(k_loc, n_rows)
+        mk(4)
+        if (f0 * R, f1 * R) == (r0, r1):
+            fbits = bits
+        else:  # this rank's repeats straddle other shards: regenerate their rows (Philox)
+            fbits = engine.sample_shapley(seed, (f1 - f0) * R, S, dev, row_offset=f0 * R)
+        st = torch.empty(1, dtype=torch.int32, device=dev)
+        w, _, _, _, _ = engine.wlm_fit(fbits.view(f1 - f0, R, -1), S, batch,
+                                       y[f0 * R:f1 * R].view(f1 - f0, R),
+                                       k[f0 * R:f1 * R].view(f1 - f0, R), w0[f0:f1], params,
+                                       check=False, status=st)
+        statuses.append(st)
+        mk(5)
+        if record:
+            for j, name in enumerate(phases):
+                ev[name].append((marks[j], marks[j + 1]))
+        w_all = sharding.gather_rows(w.reshape(f1 - f0, S), times)
+        return w_all.mean(0), w_all.std(0, unbiased=False)
+
+    for i in range(args.warmup):
+        step(i, False)
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, True)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    for st in statuses:  # outside the timed region: every fit's exchange status must be clean
+        engine.check_fit_status(st)
+    phase_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+    total_rows = n_rows * args.steps
+    ops = args.warmup + args.steps
+    wl = wlm_bytes(R, S, batch) * (f1 - f0)
+    line = {
+        "metric": METRIC,
+        "value": total_rows / elapsed,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {"workload": "c2 (BASELINE configs[1]): synthetic homogeneous 100k nodes / 1M "
+                               "edges, 64-dim feats, 2-layer GCN, interpret_samples=256, "
+                               "node_prediction (3-hop computational subgraph of node 7)",
+                   "nodes": args.nodes, "edges": args.edges, "feat": args.feat,
+                   "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
+                   "interpret_samples": args.interpret_samples, "epochs": args.epochs,
+                   "rows_per_repeat": R, "repeats_per_step": times,
+                   "parallelism": f"dp{world}: rows of the step's {times} repeat(s) sharded over "
+                                  "ranks, RCCL all-gather of logits + kernel weights, fits "
+                                  "sharded by repeat",
+                   "mask_sampler": "device (Philox Shapley)"},
+        "phases_ms": phase_ms,
+        "roofline": dict(roofline(wl, phase_ms["wlm"] * 1e-3, "headline", WLM_KERNELS, ops),
+                         kernel="surrogate fit chain (" + ", ".join(WLM_KERNELS) + ")",
+                         note="latency-bound (51 sequential Adam steps, SURVEY.md §8d regime "
+                              "(i)); the HBM fraction is reported, not the bound"),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_c2(args, arch, sub_feat, sub_ei, q)
+    del plan
+    return line
 
 
-def cpu_baseline(args, arch, sub_feat, sub_ei, q):
-    """The numpy oracle (CPU restatement of the reference path, 1 thread) on a bounded sample
-    of the same workload: cpu_rows mask rows through forward + KernelSHAP + surrogate."""
+def _c2_cpu_worker(task):
+    """Worker (spawned process, numpy only, 1 BLAS thread): oracle forward of a row chunk."""
     import oracle
-    try:
-        from threadpoolctl import threadpool_limits
-    except Exception:  # pragma: no cover
-        threadpool_limits = None
+    from threadpoolctl import threadpool_limits
+    spec, x, ei, m, q = task
+    with threadpool_limits(limits=1):
+        return oracle.masked_query_outputs(spec, x, {None: ei}, m, q, dtype=np.float32)
+
+
+def cpu_baseline_c2(args, arch, sub_feat, sub_ei, q):
+    """The numpy oracle (CPU restatement of the reference path) on the host cores: cpu_rows mask
+    rows of the same workload, the union-graph forward split over worker processes, then
+    KernelSHAP and the (sequential) surrogate fit."""
+    import oracle
     S = sub_feat.shape[0]
     rows = args.cpu_rows
     rng = np.random.default_rng(0)
@@ -163,26 +326,28 @@ def cpu_baseline(args, arch, sub_feat, sub_ei, q):
                       for i in range(2)],
             "fc": [{"W": arch.fc[0].weight.detach().cpu().numpy(),
                     "b": arch.fc[0].bias.detach().cpu().numpy(), "act": "sigmoid"}]}
-    x = sub_feat.cpu().numpy()
-    e = {None: sub_ei.cpu().numpy()}
-    ctx = threadpool_limits(limits=1) if threadpool_limits else None
-    try:
+    x, e = sub_feat.cpu().numpy(), sub_ei.cpu().numpy()
+    procs = cpu_procs(args)
+    chunks = [(spec, x, e, m[c], q) for c in np.array_split(np.arange(rows), procs * 4)]
+    with _pool(procs) as pool:
+        pool.map(_c2_cpu_worker, chunks[:procs])  # start-up (imports) outside the timing
         t0 = time.perf_counter()
-        y = oracle.masked_query_outputs(spec, x, e, m, q, dtype=np.float32)
+        y = np.concatenate(pool.map(_c2_cpu_worker, chunks))
         k = oracle.shap_kernel(m)
         oracle.train_wlm(m, args.interpret_samples, y, k, np.zeros(S, np.float32),
                          {"lr": 0.01, "l1_lambda": 1e-4}, dtype=np.float32)
         dt = time.perf_counter() - t0
-    finally:
-        if ctx is not None:
-            ctx.unregister() if hasattr(ctx, "unregister") else None
-    return {"value": rows / dt, "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": f"{rows} mask rows of the same workload (S={S}) through the numpy oracle "
-                      f"(union-graph forward + KernelSHAP + surrogate fit), {dt:.1f} s"}
+    model, ncpu = host_info()
+    return {"value": rows / dt, "unit": "samples/s", "cores": procs, "kind": "port",
+            "host_cpu": model, "host_logical_cpus": ncpu,
+            "sample": f"{rows} mask rows of the same workload (S={S}) through the numpy oracle: "
+                      f"union-graph forward over {procs} worker processes (1 thread each), "
+                      f"KernelSHAP, surrogate fit; {dt:.1f} s"}
 
 
+# ----------------------------------------------------------------------------- c3 (north star)
 def c3_graph(dev, nodes=1_000_000, edges=10_000_000, feat=128, seed=0):
-    """synthetic homogeneous graph, 2-layer SAGEConv(mean) 128-128-128, head
+    """configs[2] graph: synthetic homogeneous, 2-layer SAGEConv(mean) 128-128-128, head
     Linear(128, 1) + sigmoid (random init, ConvStack layout of the reference tests)."""
     from bikg_graph_explainability_public_amd.nn import ConvStack
     g = torch.Generator().manual_seed(seed)
@@ -193,101 +358,272 @@ def c3_graph(dev, nodes=1_000_000, edges=10_000_000, feat=128, seed=0):
     return x, ei, arch
 
 
-def full_graph_bytes(n, e_kept_per_row, e, f_in, f_out, rows, layers=2):
+def full_graph_alg_bytes(n, e_kept_per_row, e, f_in, f_out, rows, layers=2):
     """SURVEY.md §8d algorithmic bytes per sample of the full-graph masked forward, summed over
-    the rows: per layer 4(N+1) + 4E (CSR) + N/8 (mask bits) + 4 F_g E_kept (gathered rows,
-    F_g = min(F_in, F_out)) + 4 F_root N (SAGE self rows) + 4 F_out N (layer output)."""
-    per_layer_fixed = 4 * (n + 1) + 4 * e + n / 8 + 4 * f_in * n + 4 * f_out * n
-    return layers * (per_layer_fixed * rows + 4 * min(f_in, f_out) * e_kept_per_row.sum())
+    the rows; per layer 4(N+1) + 4E (CSR) + N/8 (mask bits) + 4 F_g E_kept (gathered rows,
+    F_g = min(F_in, F_out)) + 4 F_root N (SAGE self rows) + 4 F_out N (layer output).
+    Returns (total, per layer)."""
+    per_layer = 4 * (n + 1) * rows + 4 * e * rows + n / 8 * rows + \
+        4 * min(f_in, f_out) * float(np.sum(e_kept_per_row)) + 4 * f_in * n * rows + \
+        4 * f_out * n * rows
+    return layers * per_layer, per_layer
 
 
-def full_graph_section(args, dev):
-    """Regime (ii): every node a target of the masked forward on the c3 graph
-    (1M nodes / 10M edges / 128 features / 2-layer SAGE), `rows` mask rows (32-sample passes)."""
-    from bikg_graph_explainability_public_amd import engine, pipeline
+C3_KERNELS = ("k_wide_bits", "k_wide_f0", "k_wide_degree", "k_wide_tgt")
+
+
+def c3_section(args, dev, world, rank):
+    """Regime (ii) on configs[2]: every node a target of the masked forward,
+    c3_rows mask rows sharded over the ranks in 32-row passes (strong scaling), then the RCCL
+    all-gather of 64 query columns' logits of every row (what the surrogate fits consume)."""
+    from bikg_graph_explainability_public_amd import engine, pipeline, sharding
     x, ei, arch = c3_graph(dev)
     N, E = x.shape[0], ei.shape[1]
-    xd, eid = x.to(dev), ei.to(dev)
-    arch = arch.to(dev)
-    plan = pipeline.build_plan(arch, xd, eid, list(range(N)))
-    rows = args.full_graph_rows
-    bits = engine.sample_shapley(77, rows, N, dev)
-    y = plan.forward(bits)  # warm-up (workspace, code objects)
-    torch.cuda.synchronize()
+    eid = ei.to(dev)
+    plan = pipeline.build_plan(arch.to(dev), x.to(dev), eid, list(range(N)))
+    total = args.c3_rows
+    # shard in whole 32-sample passes where possible
+    passes = -(-total // 32)
+    p0, p1 = sharding.shard_range(passes, world, rank)
+    r0, r1 = min(total, 32 * p0), min(total, 32 * p1)
+    bits = engine.sample_shapley(77, r1 - r0, N, dev, row_offset=r0)
+    qcols = torch.arange(7, N, N // 64, device=dev)[:64]
     stream = torch.cuda.current_stream()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    plan.forward(bits)  # warm-up (workspace, code objects); counted in the PMC ops
     reps = 3
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world)
+    t0 = time.perf_counter()
     a.record(stream)
     for _ in range(reps):
         y = plan.forward(bits)
     b.record(stream)
+    logits = y[:, qcols] if world == 1 else _gather_uneven(y[:, qcols].contiguous(), world)
     torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / reps
-    # kept edges per row (both endpoints active), for the algorithmic byte count
-    m = engine.unpack_masks(bits, N)
-    kept = (m[:, eid[0]] & m[:, eid[1]]).sum(1).double().cpu().numpy()
-    del m
-    bytes_ = full_graph_bytes(N, kept, E, 128, 128, rows)
-    flops = rows * N * 2.0 * (2 * 128 * 128 + 128)  # layer-2 dense (l and r) + head, per target
-    achieved = bytes_ / (ms * 1e-3) / 1e9
-    passes = -(-rows // 32)
-    traffic = pmc_traffic_counts({"k_wide_bits": passes, "k_wide_f0": passes,
-                                  "k_wide_degree": passes, "k_wide_tgt<8, false": passes,
-                                  "k_wide_tgt<8, true": passes}) if rows == 64 else None
+    barrier(world)
+    wall = max_over_ranks((time.perf_counter() - t0) / reps, world, dev)
+    fwd_ms = a.elapsed_time(b) / reps
+    assert logits.shape == (total, qcols.numel())
+    # kept edges per row (both endpoints active), chunked, for the algorithmic byte count
+    kept = []
+    for c0 in range(0, r1 - r0, 32):
+        m = engine.unpack_masks(bits[c0:c0 + 32], N)
+        kept.append((m[:, eid[0]] & m[:, eid[1]]).sum(1).double().cpu().numpy())
+        del m
+    kept = np.concatenate(kept) if kept else np.zeros(0)
+    alg, per_layer = full_graph_alg_bytes(N, kept, E, 128, 128, r1 - r0)
+    flops = (r1 - r0) * N * 2.0 * (2 * 128 * 128 + 128)  # layer-2 dense (l and r) + head
+    rows_rank = r1 - r0
     out = {
-        "workload": "c3 full-graph masked forward (SURVEY.md §8d regime (ii)): 1M nodes / 10M "
-                    "edges, 128 feats, 2-layer SAGEConv(mean) + Linear(128,1) + sigmoid, every "
-                    "node a target (all 1M outputs per mask row)",
-        "rows": rows, "ms": ms, "ms_per_row": ms / rows,
-        "samples_per_s": rows / (ms * 1e-3),
-        "node_outputs_per_s": rows * N / (ms * 1e-3),
-        "roofline": {"kernel": "wide forward chain (k_wide_bits, k_wide_f0, k_wide_tgt<layer 1>, "
-                               "k_wide_tgt<layer 2 + head>)",
-                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": bytes_,
-                     "traffic": traffic,
-                     "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
-                     "bytes_formula": "SURVEY.md §8d B_alg per sample, E_kept measured per row"},
-        "mfma": {"tflops": flops / (ms * 1e-3) / 1e12, "peak_fp32_tflops": 157.3,
-                 "frac": flops / (ms * 1e-3) / 1e12 / 157.3},
+        "workload": "c3 (BASELINE configs[2]) full-graph masked forward (SURVEY.md §8d regime "
+                    "(ii)): 1M nodes / 10M edges, 128 feats, 2-layer SAGEConv(mean) + "
+                    "Linear(128,1) + sigmoid, every node a target (all 1M outputs per mask row), "
+                    f"{total} mask rows sharded over {world} rank(s) in 32-row passes, then an "
+                    "all-gather of 64 query columns of every row",
+        "rows": total, "rows_per_rank": rows_rank, "ms": wall * 1e3,
+        "forward_ms_rank0": fwd_ms,
+        "samples_per_s": total / wall,
+        "samples_per_s_per_rank": rows_rank / (fwd_ms * 1e-3),
+        "node_outputs_per_s": total * N / wall,
+        "scaling": "strong",
+        "roofline": dict(roofline(alg, fwd_ms * 1e-3, "c3", C3_KERNELS, reps + 1),
+                         kernel="wide forward chain (" + ", ".join(C3_KERNELS) + ")",
+                         bytes_formula="SURVEY.md §8d B_alg per sample, E_kept measured per row",
+                         alg_bytes_per_layer=per_layer),
+        "mfma": {"tflops": flops / (fwd_ms * 1e-3) / 1e12, "peak_fp32_tflops": FP32_MFMA_PEAK_TF,
+                 "frac": flops / (fwd_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF},
     }
-    if not args.no_cpu_baseline:
-        out["cpu_baseline"] = full_graph_cpu(arch)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_c3(args)
+    del plan, y
+    torch.cuda.empty_cache()
     return out
 
 
-def full_graph_cpu(arch):
-    """The numpy oracle (1 thread) on ONE mask row of the same model on a 1/10-scale c3 graph
-    (100k nodes / 1M edges, same degree and widths): the forward is linear in N and E, so the
-    per-sample rate at full scale is the measured one / 10 (reported as such)."""
+def _gather_uneven(t, world):
+    """All-gather of per-rank row blocks of different sizes (pads to the largest)."""
+    import torch.distributed as dist
+    n = torch.tensor([t.shape[0]], device=t.device)
+    sizes = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    cap = max(sizes)
+    buf = t.new_zeros((cap,) + tuple(t.shape[1:]))
+    buf[:t.shape[0]] = t
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf)
+    return torch.cat([o[:s] for o, s in zip(outs, sizes)])
+
+
+def _c3_cpu_worker(seed):
+    """Worker (spawned, numpy oracle, 1 BLAS thread): ONE full-size c3 mask row — the graph and
+    the model are regenerated from their seeds (same as the GPU run), every node an output."""
     import oracle
-    try:
-        from threadpoolctl import threadpool_limits
-    except Exception:  # pragma: no cover
-        threadpool_limits = None
-    x, ei, _ = c3_graph("cpu", nodes=100_000, edges=1_000_000)
-    sd = {k: v.detach().cpu().numpy() for k, v in arch.state_dict().items()}
+    from threadpoolctl import threadpool_limits
+    x, ei, arch = c3_graph("cpu")
+    sd = {k: v.detach().numpy() for k, v in arch.state_dict().items()}
     spec = {"convs": [{"kind": "sage", "rels": [None], "act": "relu",
                        "params": {None: {"Wl": sd[f"conv.{2 * i}.lin_l.weight"],
                                          "bl": sd[f"conv.{2 * i}.lin_l.bias"],
                                          "Wr": sd[f"conv.{2 * i}.lin_r.weight"]}}}
                       for i in range(2)],
             "fc": [{"W": sd["fc.0.weight"], "b": sd["fc.0.bias"], "act": "sigmoid"}]}
-    rng = np.random.default_rng(0)
-    m = rng.random(x.shape[0]) < 0.5
-    e = ei.numpy()
+    xn, e = x.numpy(), ei.numpy()
+    m = np.random.default_rng(seed).random(xn.shape[0]) < 0.5
     keep = m[e[0]] & m[e[1]]
-    ctx = threadpool_limits(limits=1) if threadpool_limits else None
-    try:
+    with threadpool_limits(limits=1):
         t0 = time.perf_counter()
-        oracle.forward_union(spec, x.numpy(), {None: (e[0][keep], e[1][keep])}, dtype=np.float32)
+        oracle.forward_union(spec, xn, {None: (e[0][keep], e[1][keep])}, dtype=np.float32)
+        return time.perf_counter() - t0
+
+
+def cpu_baseline_c3(args):
+    """The numpy oracle on the host cores: one full-size c3 mask row (1M nodes / 10M edges, every
+    node an output) per worker process, all workers at once."""
+    procs = cpu_procs(args)
+    with _pool(procs) as pool:
+        t0 = time.perf_counter()
+        per = pool.map(_c3_cpu_worker, list(range(procs)))
         dt = time.perf_counter() - t0
-    finally:
-        if ctx is not None and hasattr(ctx, "unregister"):
-            ctx.unregister()
-    return {"value": 1.0 / (dt * 10), "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": f"1 mask row through the numpy oracle on a 1/10-scale c3 graph (100k nodes / "
-                      f"1M edges) in {dt:.1f} s; full-scale rate = 1 / (10 x {dt:.1f} s)"}
+    model, ncpu = host_info()
+    return {"value": procs / max(per), "unit": "samples/s", "cores": procs, "kind": "port",
+            "host_cpu": model, "host_logical_cpus": ncpu,
+            "sample": f"{procs} full-size mask rows, one per worker process (1 thread each, all "
+                      f"concurrent), through the numpy oracle's union-graph forward: "
+                      f"{np.mean(per):.1f} s mean / {max(per):.1f} s max forward per row "
+                      f"(value = rows / max); {dt:.1f} s wall incl. graph generation"}
+
+
+# ----------------------------------------------------------------------------- c5
+C5_RELS = [("gene", "interacts", "gene"), ("gene", "encodes", "protein"),
+           ("protein", "binds", "protein"), ("drug", "targets", "protein"),
+           ("protein", "regulates", "gene")]
+
+
+def c5_section(args, dev, world, rank):
+    """configs[4]: 1M-node heterogeneous graph (500k gene / 300k protein / 200k drug, 256-dim
+    features each), 5 relations (3 bipartite), 10M edges, 2-layer HeteroConv(SAGE) 256 -> 64 ->
+    64 + head 64 -> 16 -> 1 + sigmoid, node_prediction of gene 7 (the L+1-hop subgraph by the HIP
+    k-hop kernel), 20 random communities over the subgraph, device community sampler,
+    interpret_samples=1024 x epochs=50, repeats=10, the reference's Q4 targets, community scores.
+    One step = the whole 10-repeat job as Explainer.run shards it: every rank draws the masks
+    (replicated sampler), forwards + KernelSHAPs its shard of the 10 x R rows, all-gathers the
+    logits and kernel weights, fits its share of the repeats in one batched launch,
+    all-gathers the weights, then mean / std and the community means."""
+    from bikg_graph_explainability_public_amd import engine, pipeline, sharding
+    from bikg_graph_explainability_public_amd.data import Data
+    from bikg_graph_explainability_public_amd.masks import Mask
+    from bikg_graph_explainability_public_amd.nn import HeteroSageStack
+    from bikg_graph_explainability_public_amd.pathways import Pathways
+    sizes = {"gene": 500_000, "protein": 300_000, "drug": 200_000}
+    F = 256
+    g = torch.Generator(device=dev).manual_seed(5)
+    feat = {t: torch.randn((n, F), generator=g, device=dev) for t, n in sizes.items()}
+    ei = {r: torch.stack([torch.randint(0, sizes[r[0]], (2_000_000,), generator=g, device=dev),
+                          torch.randint(0, sizes[r[-1]], (2_000_000,), generator=g, device=dev)])
+          for r in C5_RELS}
+    torch.manual_seed(0)
+    arch = HeteroSageStack(C5_RELS, {t: F for t in sizes}, 64, 2, [64, 16, 1]).to(dev).eval()
+    fh, eh, nt, et, _, _, pads = Data(feat, ei).hetero2homo()
+    ntn, etn = list(feat), list(ei)
+    del feat, ei
+    sub_x, sub_ei, _, sub_ind, sub_nt, sub_et = Data(fh, eh).comp_graph(
+        7, 2, "node", [str(i) for i in range(fh.shape[0])], nt, et)
+    del fh, eh, nt, et
+    sub_nt = sub_nt.long()
+    q = int(sub_ind)
+    plan = pipeline.build_plan(arch, sub_x, sub_ei, [q], sub_nt, sub_et, ntn, etn, pads)
+    assert plan is not None and plan.multi_type
+    S = sub_x.shape[0]
+    rng = np.random.default_rng(20)
+    cuts = np.sort(rng.choice(np.arange(1, S), 19, replace=False))
+    pathways = [sorted(c.tolist()) for c in np.split(rng.permutation(S), cuts)]
+    epochs, times = 50, args.c5_times
+    params = {"interpret_samples": args.c5_samples, "epochs": epochs, "lr": 0.01,
+              "l1_lambda": 1e-4}
+    cplan = Mask(sub_x, sub_ei, pathways, params, "node_prediction").community_plan()
+    tabs = engine.community_tables(cplan, pathways, S, dev)
+    R = cplan[2]
+    batch = R // epochs
+    n_rows = times * R
+    r0, r1 = sharding.shard_range(n_rows, world, rank)
+    f0, f1 = sharding.shard_range(times, world, rank)
+    w0 = torch.zeros((times, S), device=dev)
+    fit = {"lr": 0.01, "l1_lambda": 1e-4}
+    pw = Pathways(pathways, [f"community_{i}" for i in range(20)])
+    stream = torch.cuda.current_stream()
+    statuses = []
+    phases = ("sample", "forward", "shap", "gather", "wlm", "scores")
+    ev = {k: [] for k in phases}
+
+    def job(step_seed, record):
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
+        mk = (lambda j: marks[j].record(stream)) if record else (lambda j: None)
+        mk(0)
+        bits = torch.stack([engine.sample_communities(step_seed * 100 + i, cplan, pathways, S,
+                                                      dev, tables=tabs)[0]
+                            for i in range(times)])              # [times, R, W] (replicated)
+        flat = bits.view(n_rows, -1)
+        mk(1)
+        y_loc = plan.forward(flat[r0:r1])[:, 0]
+        empty = pipeline.empty_copy_rows(flat[r0:r1], S, sub_ei)
+        mk(2)
+        k_loc = engine.shap_kernel(flat[r0:r1], S)
+        mk(3)
+        y = sharding.gather_rows(y_loc, n_rows).view(times, R)
+        empty = sharding.gather_rows(empty, n_rows).view(times, R)
+        k = sharding.gather_rows(k_loc, n_rows).view(times, R)
+        y = torch.stack([pipeline.multi_type_targets(y[i], empty[i], batch, q, S, q4=True)
+                         for i in range(f0, f1)]) if f1 > f0 else y[:0]
+        mk(4)
+        st = torch.empty(1, dtype=torch.int32, device=dev)
+        if f1 > f0:
+            w, _, _, _, _ = engine.wlm_fit(bits[f0:f1], S, batch, y, k[f0:f1], w0[f0:f1], fit,
+                                           check=False, status=st)
+            statuses.append(st)
+        else:
+            w = torch.empty((0, S), device=dev)
+        w_all = sharding.gather_rows(w, times)
+        mean, std = w_all.mean(0), w_all.std(0, unbiased=False)
+        mk(5)
+        pdf = pw.aggregate(mean, pathways)  # device segmented mean + DataFrame (host sync)
+        mk(6)
+        if record:
+            for j, name in enumerate(phases):
+                ev[name].append((marks[j], marks[j + 1]))
+        return mean, std, pdf
+
+    job(0, False)
+    reps = 2
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(reps):
+        job(1 + i, True)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = max_over_ranks((time.perf_counter() - t0) / reps, world, dev)
+    for st in statuses:
+        engine.check_fit_status(st)
+    ph = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
+    out = {"workload": "c5 (BASELINE configs[4]): 1M-node hetero graph (3 node types, 256-dim "
+                       "feats, 5 relations / 10M edges), 2-layer HeteroConv(SAGE) 256->64->64 + "
+                       "head 64->16->1, node_prediction of gene 7, 20 random communities, device "
+                       f"community sampler, interpret_samples={args.c5_samples} x epochs=50, "
+                       f"repeats={times}, reference Q4 targets, community scores",
+           "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
+           "rows_per_repeat": R, "repeats": times, "rows_per_job": n_rows,
+           "ms_per_job": wall * 1e3, "samples_per_s": n_rows / wall,
+           "phases_ms_rank0": ph, "scaling": "strong",
+           "parallelism": f"{world} rank(s): rows of the {times} repeats sharded, RCCL "
+                          "all-gather of logits / kernel weights, fits sharded by repeat "
+                          "(batched launch per rank)"}
+    del plan
+    torch.cuda.empty_cache()
+    return out
+
+
+# ----------------------------------------------------------------------------- N = 1 sections
+GP_KERNELS = ("k_wlm_stats", "k_gw_p", "k_gw_g", "k_gw_grad", "k_gw_loss", "k_argmin_first")
 
 
 def graph_prediction_section(args, dev):
@@ -306,20 +642,16 @@ def graph_prediction_section(args, dev):
     stream = torch.cuda.current_stream()
 
     def rep(i, ev=None):
-        if ev:
-            ev[0].record(stream)
+        mk = (lambda j: ev[j].record(stream)) if ev else (lambda j: None)
+        mk(0)
         bits, cnt = engine.sample_shapley(500 + i, R, N, dev, with_counts=True)
-        if ev:
-            ev[1].record(stream)
+        mk(1)
         y = plan.forward(bits)[:, 0]
-        if ev:
-            ev[2].record(stream)
+        mk(2)
         k = engine.shap_kernel(bits, N, counts=cnt)
-        if ev:
-            ev[3].record(stream)
-        engine.wlm_fit(bits, N, batch, y, k, w0, params)
-        if ev:
-            ev[4].record(stream)
+        mk(3)
+        engine.wlm_fit(bits, N, batch, y, k, w0, params, check=False)
+        mk(4)
 
     rep(0)
     torch.cuda.synchronize()
@@ -333,26 +665,14 @@ def graph_prediction_section(args, dev):
     total = sum(ph.values())
     W = (N + 31) // 32
     wbytes = 2 * R * W * 4 + epochs * 6 * N * 4  # mask bits twice per step + Adam state r/w
-    traffic = pmc_traffic_counts({"k_gw_p": epochs, "k_gw_g": epochs, "k_gw_grad": epochs,
-                                  "k_gw_loss": 1})
     return {"workload": "c3 graph_prediction, one query (node 7), S = 1M mask columns, "
                         "interpret_samples=512 x epochs=50 = 25,600 rows, one repeat",
             "ms_per_repeat": total, "samples_per_s": R / (total * 1e-3), "phases_ms": ph,
-            "roofline": {"kernel": "many-column surrogate fit (k_wlm_stats, k_gw_p, k_gw_g, "
-                                   "k_gw_grad, k_gw_loss)", "bound": "hbm",
-                         "achieved": wbytes / (ph["wlm"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s",
-                         "frac": wbytes / (ph["wlm"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "bytes_per_launch": wbytes, "traffic": traffic,
-                         "traffic_source": "profiles/pmc_traffic.json" if traffic else None,
-                         "bytes_formula": "2 x R x ceil(S/32) x 4 (bits, p and grad passes) + "
-                                          "steps x 24 S (w, m, v read + write)"},
+            "roofline": dict(roofline(wbytes, ph["wlm"] * 1e-3, "gp", GP_KERNELS, reps + 1),
+                             kernel="many-column surrogate fit (" + ", ".join(GP_KERNELS) + ")",
+                             bytes_formula="2 x R x ceil(S/32) x 4 (bits, p and grad passes) + "
+                                           "steps x 24 S (w, m, v read + write)"),
             "sampler_GBps": R * W * 4 / (ph["sample"] * 1e-3) / 1e9}
-
-
-C4_RELS = [("gene", "interacts", "gene"), ("gene", "encodes", "protein"),
-           ("protein", "binds", "protein"), ("drug", "targets", "protein"),
-           ("protein", "regulates", "gene")]
 
 
 def hetero_c4_section(args, dev):
@@ -361,10 +681,11 @@ def hetero_c4_section(args, dev):
     (gcn_hetero_1hop shape: 84 -> 16, head 16 -> 16 -> 32 -> 1; GCNConv cannot take bipartite
     relations), node_prediction of gene 7 through Explainer's host steps (hetero2homo, k-hop
     subgraph on the GPU), then per repeat: device Shapley masks -> node-type-gated forward ->
-    empty-copy / Q4 targets -> KernelSHAP -> surrogate fit.  Regime (i): the subgraph is
-    cache-resident, so samples/s is the figure (no HBM fraction).  `reference_loop` times the
-    reference's own per-copy multi-type loop (model.py:196-249, one arch call + host sync per
-    row) on the same GPU for one batch."""
+    empty-copy / Q4 targets -> KernelSHAP -> surrogate fit, in the reference's semantics
+    (hetero_q4=True: quirk Q4) and with per-copy targets (hetero_q4=False).  Regime (i): the
+    subgraph is cache-resident, so samples/s is the figure (no HBM fraction).
+    `reference_loop` times the reference's own per-copy multi-type loop (model.py:196-249, one
+    arch call + host sync per row) on the same GPU for one batch."""
     from bikg_graph_explainability_public_amd import engine, pipeline
     from bikg_graph_explainability_public_amd.data import Data
     from bikg_graph_explainability_public_amd.model import Model
@@ -375,9 +696,9 @@ def hetero_c4_section(args, dev):
     feat = {t: torch.randn((n, dims[t]), generator=g, device=dev) for t, n in sizes.items()}
     ei = {r: torch.stack([torch.randint(0, sizes[r[0]], (1_000_000,), generator=g, device=dev),
                           torch.randint(0, sizes[r[-1]], (1_000_000,), generator=g, device=dev)])
-          for r in C4_RELS}
+          for r in C5_RELS}
     torch.manual_seed(0)
-    arch = HeteroSageStack(C4_RELS, dims, 16, 1, [16, 16, 32, 1]).to(dev).eval()
+    arch = HeteroSageStack(C5_RELS, dims, 16, 1, [16, 16, 32, 1]).to(dev).eval()
     d = Data(feat, ei)
     fh, eh, nt, et, _, _, pads = d.hetero2homo()
     ntn, etn = list(feat), list(ei)
@@ -397,60 +718,77 @@ def hetero_c4_section(args, dev):
     params = {"lr": 0.01, "l1_lambda": 1e-4}
     w0 = torch.zeros(S, device=dev)
     stream = torch.cuda.current_stream()
+    out = {"workload": "c4: 3 node types (200k/200k/100k, 84/64/32 feats), 5 relations (3 "
+                       "bipartite), 5M edges, HeteroConv(SAGE) 1 layer 84->16 + head "
+                       "16->16->32->1, node_prediction of gene 7, interpret_samples=256 x "
+                       "epochs=50 = 12,800 rows, one repeat",
+           "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
+           "khop_ms": t_khop * 1e3}
+    for q4 in (True, False):
+        if q4:
+            # the reference's Q4 extraction keeps out[sub_ind::S] of each batch of copies: with
+            # batch > S it keeps several values, which weighted_mse_loss cannot broadcast against
+            # the [batch] prediction — the reference fails on this configuration
+            ncut = len(range(q, batch, S))
+            if ncut not in (1, batch):
+                out["q4_true"] = {
+                    "semantics": "reference (quirk Q4)",
+                    "result": f"not runnable in the reference: batch {batch} > subgraph {S} "
+                              f"nodes, so each batch's extraction out[{q}::{S}] keeps {ncut} "
+                              "values and weighted_mse_loss (wlm.py:517) cannot broadcast "
+                              f"them against the {batch} predictions; the engine raises the "
+                              "same error (pipeline.multi_type_targets)"}
+                continue
 
-    def rep(i, ev=None):
-        if ev:
-            ev[0].record(stream)
-        bits, cnt = engine.sample_shapley(900 + i, R, S, dev, with_counts=True)
-        if ev:
-            ev[1].record(stream)
-        y = plan.forward(bits)[:, 0]
-        empty = pipeline.empty_copy_rows(bits, S, sub_ei)
-        y = pipeline.multi_type_targets(y, empty, batch, q, S, q4=False)
-        if ev:
-            ev[2].record(stream)
-        k = engine.shap_kernel(bits, S, counts=cnt)
-        if ev:
-            ev[3].record(stream)
-        engine.wlm_fit(bits, S, batch, y, k, w0, params)
-        if ev:
-            ev[4].record(stream)
+        def rep(i, ev=None):
+            mk = (lambda j: ev[j].record(stream)) if ev else (lambda j: None)
+            mk(0)
+            bits, cnt = engine.sample_shapley(900 + i, R, S, dev, with_counts=True)
+            mk(1)
+            y = plan.forward(bits)[:, 0]
+            empty = pipeline.empty_copy_rows(bits, S, sub_ei)
+            y = pipeline.multi_type_targets(y, empty, batch, q, S, q4=q4)
+            mk(2)
+            k = engine.shap_kernel(bits, S, counts=cnt)
+            mk(3)
+            engine.wlm_fit(bits, S, batch, y, k, w0, params, check=False)
+            mk(4)
 
-    rep(0)
-    torch.cuda.synchronize()
-    reps = 5
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(reps)]
-    t0 = time.perf_counter()
-    for i in range(reps):
-        rep(1 + i, evs[i])
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / reps
-    ph = {name: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in evs]))
-          for j, name in enumerate(("sample", "forward", "shap", "wlm"))}
+        rep(0)
+        torch.cuda.synchronize()
+        reps = 5
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(reps)]
+        t0 = time.perf_counter()
+        for i in range(reps):
+            rep(1 + i, evs[i])
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / reps
+        ph = {name: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in evs]))
+              for j, name in enumerate(("sample", "forward", "shap", "wlm"))}
+        out["q4_true" if q4 else "q4_false"] = {
+            "semantics": "reference (quirk Q4: each batch's targets collapse to out[sub_ind])"
+                         if q4 else "per-copy targets (hetero_q4=False)",
+            "ms_per_repeat": wall * 1e3, "samples_per_s": R / wall, "phases_ms": ph}
+    out["samples_per_s"] = out["q4_true"].get("samples_per_s", out["q4_false"]["samples_per_s"])
     # the reference's per-copy loop on the same GPU, one batch of rows
     mask = engine.unpack_masks(engine.sample_shapley(77, batch, S, dev), S)
     cf, cnt_t, pei, pet = Data(sub_x, sub_ei).perturbator(mask, "node", sub_nt, sub_et)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    Model(arch).predict_hetero_output(cf, pei.long(), cnt_t, pet, ntn, etn, batch, S, q, pads, "node")
+    Model(arch).predict_hetero_output(cf, pei.long(), cnt_t, pet, ntn, etn, batch, S, q, pads,
+                                      "node")
     torch.cuda.synchronize()
-    loop_rate = batch / (time.perf_counter() - t0)
-    return {"workload": "c4: 3 node types (200k/200k/100k, 84/64/32 feats), 5 relations (3 "
-                        "bipartite), 5M edges, HeteroConv(SAGE) 1 layer 84->16 + head "
-                        "16->16->32->1, node_prediction of gene 7, interpret_samples=256 x "
-                        "epochs=50 = 12,800 rows, one repeat, per-copy targets (hetero_q4=False)",
-            "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
-            "khop_ms": t_khop * 1e3, "ms_per_repeat": wall * 1e3,
-            "samples_per_s": R / wall, "phases_ms": ph,
-            "reference_loop_gpu_samples_per_s": loop_rate}
+    out["reference_loop_gpu_samples_per_s"] = batch / (time.perf_counter() - t0)
+    return out
 
 
-def communities_section(args, dev, plan, sub_feat, sub_ei, reps=10):
+def communities_section(args, dev, reps=10):
     """c2 with 20 random communities over the subgraph (SURVEY.md §8d c5-style communities):
     the device community sampler (k_communities) inside the full repeat pipeline, and the
     compat CPU sampler (the reference's masks.py:262-397 algorithm and RNG order) beside it."""
     from bikg_graph_explainability_public_amd import engine
     from bikg_graph_explainability_public_amd.masks import Mask
+    arch, sub_feat, sub_ei, q, plan = build_c2(args, dev)
     S = plan.cols
     rng = np.random.default_rng(20)
     cuts = np.sort(rng.choice(np.arange(1, S), 19, replace=False))
@@ -469,7 +807,8 @@ def communities_section(args, dev, plan, sub_feat, sub_ei, reps=10):
         bits, _ = engine.sample_communities(4000 + i, cplan, pathways, S, dev, tables=tabs)
         y = plan.forward(bits)[:, 0]
         k = engine.shap_kernel(bits, S)
-        return engine.wlm_fit(bits.view(1, R, -1), S, batch, y.view(1, R), k.view(1, R), w0, fit)
+        return engine.wlm_fit(bits.view(1, R, -1), S, batch, y.view(1, R), k.view(1, R), w0,
+                              fit, check=False)
 
     rep(0)
     torch.cuda.synchronize()
@@ -535,143 +874,41 @@ def graph_queries_section(args, dev, n=10_000, e=100_000, f=64, queries=8):
             "speedup": t_loop / t_shared}
 
 
+# ----------------------------------------------------------------------------- main
 def main():
     args = parse()
-    world, rank, local = setup_dist(args)
+    world, rank, local = setup_dist()
     dev = torch.device("cuda", torch.cuda.current_device())
-    from bikg_graph_explainability_public_amd import _lib, engine, sharding
-
+    from bikg_graph_explainability_public_amd import _lib
     _lib.load()
-    arch, sub_feat, sub_ei, q, plan = build_workload(args, dev)
-    S = plan.cols
-    R = args.interpret_samples * args.epochs
-    batch = R // args.epochs
-    params = {"lr": 0.01, "l1_lambda": 1e-4}
-    stream = torch.cuda.current_stream()
-    ev = {k: [] for k in ("sample", "forward", "shap", "wlm")}
-
-    T = args.repeats
-    w0 = torch.zeros((T, S), device=dev)
-
-    def step(i, record):
-        marks = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
-        if record:
-            marks[0].record(stream)
-        bits = engine.sample_shapley(1000 + i * world + rank, T * R, S, dev)
-        if record:
-            marks[1].record(stream)
-        y = plan.forward(bits)[:, 0]
-        if record:
-            marks[2].record(stream)
-        k = engine.shap_kernel(bits, S)
-        if record:
-            marks[3].record(stream)
-        w, _, _, _, _ = engine.wlm_fit(bits.view(T, R, -1), S, batch, y.view(T, R),
-                                       k.view(T, R), w0, params)
-        if record:
-            marks[4].record(stream)
-            for j, name in enumerate(("sample", "forward", "shap", "wlm")):
-                ev[name].append((marks[j], marks[j + 1]))
-        if world > 1:
-            # weight_stacking (explainer.py:288-314) over every rank's repeats: one all-gather
-            w = sharding.gather_rows(w.reshape(T, S), T * world)
-        return w.mean(0), w.std(0, unbiased=False)
-
-    for i in range(args.warmup):
-        step(i, False)
-    torch.cuda.synchronize()
+    want = SECTIONS if args.sections == "all" else tuple(args.sections.split(","))
     if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    phase_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
-
-    if rank == 0:
-        total_rows = R * T * world * args.steps
-        dominant = max(phase_ms, key=phase_ms.get)
-        if dominant == "wlm":
-            bytes_launch = wlm_bytes(R, S, batch) * T
-            kname = "surrogate fit chain (k_wlm_stats, k_wlm_colbits, k_wlm_fit, k_wlm_loss)"
-            kernels = ("k_wlm_stats", "k_wlm_colbits", "k_wlm_fit", "k_wlm_loss", "k_argmin_first")
-        elif dominant == "forward":
-            bytes_launch = forward_bytes(plan, R * T)
-            kname = "masked forward chain (k_degree, k_agg, k_dense, k_take_col)"
-            kernels = ("k_degree", "k_agg", "k_dense", "k_take_col", "k_fused_forward")
-        elif dominant == "shap":
-            bytes_launch = T * R * (((S + 31) // 32) * 4 + 12)
-            kname = "k_popcount + k_shap"
-            kernels = ("k_popcount", "k_shap")
-        else:
-            bytes_launch = T * R * ((S + 31) // 32) * 4
-            kname = "k_shapley"
-            kernels = ("k_shapley",)
-        achieved = bytes_launch / (phase_ms[dominant] * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(kernels, args)
-        line = {
-            "metric": METRIC,
-            "value": total_rows / elapsed,
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic",
-            "config": {"workload": "c2: synthetic homogeneous 100k nodes / 1M edges, 64-dim "
-                                   "feats, 2-layer GCN, interpret_samples=256, node_prediction "
-                                   "(3-hop computational subgraph of node 7)",
-                       "nodes": args.nodes, "edges": args.edges, "feat": args.feat,
-                       "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
-                       "interpret_samples": args.interpret_samples, "epochs": args.epochs,
-                       "rows_per_repeat": R, "repeats_per_rank": T,
-                       "repeats_per_step": T * world,
-                       "parallelism": f"repeats sharded over {world} rank(s)",
-                       "mask_sampler": "device (Philox Shapley)"},
-            "phases_ms": phase_ms,
-            "roofline": {"kernel": kname, "bound": "hbm", "achieved": achieved,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "bytes_per_launch": bytes_launch},
-        }
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args, arch, sub_feat, sub_ei, q)
-        if world == 1:
-            comm = None if args.no_communities else communities_section(args, dev, plan, sub_feat, sub_ei)
-            del plan
+        want = tuple(s for s in want if s in MULTI_GPU_SECTIONS)
+    log(rank, f"bench: world {world}, sections {','.join(want)}")
+    line = headline(args, dev, world, rank) if "headline" in want else \
+        {"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": world,
+         "note": "headline skipped (--sections)"}
+    torch.cuda.empty_cache()
+    regimes = {}
+    runners = [("c3", "c3_full_graph", lambda: c3_section(args, dev, world, rank)),
+               ("c5", "c5_hetero", lambda: c5_section(args, dev, world, rank)),
+               ("gp", "graph_prediction_c3", lambda: graph_prediction_section(args, dev)),
+               ("c4", "hetero_c4", lambda: hetero_c4_section(args, dev)),
+               ("comm", "communities_c2", lambda: communities_section(args, dev)),
+               ("queries", "graph_queries", lambda: graph_queries_section(args, dev))]
+    for key, name, fn in runners:
+        if key in want:
+            t0 = time.perf_counter()
+            log(rank, f"section {name} ...")
+            regimes[name] = fn()
             torch.cuda.empty_cache()
-            regimes = {}
-            if not args.no_graph_prediction:
-                regimes["graph_prediction_c3"] = graph_prediction_section(args, dev)
-                torch.cuda.empty_cache()
-            if args.full_graph_rows > 0:
-                regimes["full_graph_c3"] = full_graph_section(args, dev)
-                torch.cuda.empty_cache()
-            if not args.no_hetero:
-                regimes["hetero_c4"] = hetero_c4_section(args, dev)
-                torch.cuda.empty_cache()
-            if comm is not None:
-                regimes["communities_c2"] = comm
-            if not args.no_communities:
-                regimes["graph_queries"] = graph_queries_section(args, dev)
-                torch.cuda.empty_cache()
-            if regimes:
-                line["regimes"] = regimes
+            log(rank, f"section {name} done in {time.perf_counter() - t0:.1f} s")
+    if regimes:
+        line["regimes"] = regimes
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -92,7 +92,15 @@ def multi_type_targets(y_rows, empty, batch, sub_ind, S, q4=True):
     if not q4:
         return y
     out = torch.empty_like(y)
-    for r0 in range(0, y.shape[0], batch):
+    nfull = y.shape[0] // batch
+    if nfull and sub_ind < batch <= S + sub_ind:
+        # every full batch keeps exactly one value, row sub_ind: one vectorised broadcast
+        out[:nfull * batch] = y[:nfull * batch].view(nfull, batch)[:, sub_ind:sub_ind + 1] \
+            .expand(nfull, batch).reshape(-1)
+        start = nfull * batch
+    else:
+        start = 0
+    for r0 in range(start, y.shape[0], batch):
         yb = y[r0:r0 + batch]
         sel = yb[sub_ind::S]
         if sel.numel() == yb.numel():
