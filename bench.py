@@ -131,17 +131,21 @@ def _pool(n):
     return mp.get_context("spawn").Pool(n)
 
 
-def pmc_chain(section, kernels, ops):
+def pmc_chain(section, kernels):
     """Counter-measured HBM bytes of ONE operation of a section's launch chain, from the
     section's own rocprofv3 PMC passes (profiles/pmc_<section>.json, tools/pmc_traffic.py:
     2 x FETCH_SIZE + WRITE_SIZE per dispatch, MI355X_MICROARCH.md HBM section).  `kernels` are
     exact kernel names (template arguments stripped, no prefix matching); the file's bytes of
     those kernels over all their dispatches are divided by `ops`, the number of operations
-    the section runs.  Returns (bytes per op, {kernel: bytes per op}) or (None, None)."""
+    the profiled run made (`_ops` in the file, written by the profiling script).  Returns
+    (bytes per op, {kernel: bytes per op}) or (None, None)."""
     fn = os.path.join(ROOT, "profiles", f"pmc_{section}.json")
     if not os.path.exists(fn):
         return None, None
     data = json.load(open(fn))
+    if "_ops" not in data:
+        return None, None
+    ops = data.pop("_ops")
     per = {}
     for name, d in data.items():
         base = name.split("<")[0]
@@ -152,14 +156,14 @@ def pmc_chain(section, kernels, ops):
     return sum(per.values()), per
 
 
-def roofline(alg_bytes, seconds, section=None, kernels=(), ops=1, alg_per_kernel=None):
+def roofline(alg_bytes, seconds, section=None, kernels=(), alg_per_kernel=None):
     """The roofline object of one launch chain: algorithmic bytes per op over the measured time,
     plus the counter-measured bytes (traffic) of the same op when the section's PMC file exists."""
     achieved = alg_bytes / seconds / 1e9
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "bytes_per_launch": alg_bytes, "traffic": None}
     if section is not None:
-        traffic, per = pmc_chain(section, set(kernels), ops)
+        traffic, per = pmc_chain(section, set(kernels))
         if traffic is not None:
             out["traffic"] = traffic
             out["traffic_source"] = f"profiles/pmc_{section}.json"
@@ -264,7 +268,6 @@ def headline(args, dev, world, rank):
         engine.check_fit_status(st)
     phase_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
     total_rows = n_rows * args.steps
-    ops = args.warmup + args.steps
     wl = wlm_bytes(R, S, batch) * (f1 - f0)
     line = {
         "metric": METRIC,
@@ -291,7 +294,7 @@ def headline(args, dev, world, rank):
                                   "sharded by repeat",
                    "mask_sampler": "device (Philox Shapley)"},
         "phases_ms": phase_ms,
-        "roofline": dict(roofline(wl, phase_ms["wlm"] * 1e-3, "headline", WLM_KERNELS, ops),
+        "roofline": dict(roofline(wl, phase_ms["wlm"] * 1e-3, "headline", WLM_KERNELS),
                          kernel="surrogate fit chain (" + ", ".join(WLM_KERNELS) + ")",
                          note="latency-bound (51 sequential Adam steps, SURVEY.md §8d regime "
                               "(i)); the HBM fraction is reported, not the bound"),
@@ -426,7 +429,7 @@ def c3_section(args, dev, world, rank):
         "samples_per_s_per_rank": rows_rank / (fwd_ms * 1e-3),
         "node_outputs_per_s": total * N / wall,
         "scaling": "strong",
-        "roofline": dict(roofline(alg, fwd_ms * 1e-3, "c3", C3_KERNELS, reps + 1),
+        "roofline": dict(roofline(alg, fwd_ms * 1e-3, "c3", C3_KERNELS),
                          kernel="wide forward chain (" + ", ".join(C3_KERNELS) + ")",
                          bytes_formula="SURVEY.md §8d B_alg per sample, E_kept measured per row",
                          alg_bytes_per_layer=per_layer),
@@ -668,7 +671,7 @@ def graph_prediction_section(args, dev):
     return {"workload": "c3 graph_prediction, one query (node 7), S = 1M mask columns, "
                         "interpret_samples=512 x epochs=50 = 25,600 rows, one repeat",
             "ms_per_repeat": total, "samples_per_s": R / (total * 1e-3), "phases_ms": ph,
-            "roofline": dict(roofline(wbytes, ph["wlm"] * 1e-3, "gp", GP_KERNELS, reps + 1),
+            "roofline": dict(roofline(wbytes, ph["wlm"] * 1e-3, "gp", GP_KERNELS),
                              kernel="many-column surrogate fit (" + ", ".join(GP_KERNELS) + ")",
                              bytes_formula="2 x R x ceil(S/32) x 4 (bits, p and grad passes) + "
                                            "steps x 24 S (w, m, v read + write)"),

@@ -21,10 +21,19 @@ for step in "$@"; do
     bench10) run bench10 600 python bench.py --repeats 10 --no-cpu-baseline ;;
     fwdprobe) XPG_LIB=tools/libxpgnn_stamps.so run fwdprobe 300 python tools/fwd_probe.py ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;
+    profall) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profall -o run -- python3 bench.py --no-cpu-baseline ;;
+    benchall) run benchall 900 python bench.py ;;
     prof)  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     pmc)   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline && \
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    pmc_*) # per-section PMC passes: pmc_<section> (headline: 1 warmup + 5 steps = 6 ops;
+           # c3 / gp: 1 warm-up + 3 timed forwards / repeats = 4 ops)
+           sec=${step#pmc_}
+           cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run pmc_fetch_$sec 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_$sec -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections $sec && \
+           run pmc_write_$sec 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_$sec -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections $sec ;;
   esac
 done

@@ -1,13 +1,15 @@
 """Per-kernel HBM traffic from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/r01_pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [OPS] > profiles/pmc_<section>.json
 
 Reads the `*counter_collection.csv` of each pass, sums the counter over the rows of one dispatch
 and averages over the dispatches of each kernel.  FETCH_SIZE / WRITE_SIZE are in KB
 (rocprofv3 derived counters: TCC_EA0_RDREQ/WRREQ x 64 B / 1024).  Per MI355X_MICROARCH.md
 (HBM section) FETCH_SIZE counts 128-B read requests at 64 B on gfx950, so the corrected read
 bytes are 2 x FETCH_SIZE; WRITE_SIZE is taken as is.  Output: JSON {kernel: {dispatches,
-fetch_kb_raw, write_kb, read_bytes, write_bytes, traffic_bytes}} per launch.
+fetch_kb_raw, write_kb, read_bytes, write_bytes, traffic_bytes}} per launch, plus
+`"_ops": OPS` = the number of section operations (bench repeats / steps) the profiled run made,
+so bench.py can turn dispatch totals into bytes per operation whatever its own step count.
 """
 import csv
 import glob
@@ -51,6 +53,8 @@ def main():
                       "write_kb": wk, "read_bytes": rb, "write_bytes": wb,
                       "traffic_bytes": (rb or 0) + (wb or 0) if (rb is not None or wb is not None)
                       else None}
+    if len(sys.argv) > 3:
+        res["_ops"] = int(sys.argv[3])
     json.dump(res, sys.stdout, indent=1)
     print()
 
