@@ -2098,16 +2098,28 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
 //     afterwards by k_wlm_loss from the recorded predictions and pre-step weights.
 struct WlmStep {
   double ybar, ksum, vy;
-  float step_size, bc2_sqrt;
+  double cg;  // 2 / (B sum k): the per-row gradient factor g_j = k_j cg (p_j - ybar)
+  float step_size, bc2_sqrt, inv_bc2;  // inv_bc2 = 1 / bc2_sqrt (multi-workgroup fit)
+  float pad;
 };
 
+// Also clears the multi-workgroup fit's exchange slots (`clr`, n_clr granules) and error words
+// (`clr32`, n_clr32), so the fit needs no memset launches (plain stores; the kernel boundary
+// makes them visible to the fit).
 __global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
                                                    const double* __restrict__ kern, int64_t rows,
                                                    int batch, xpg_wlm_params P, int64_t step0,
-                                                   WlmStep* __restrict__ st) {
+                                                   WlmStep* __restrict__ st, uint64_t* __restrict__ clr,
+                                                   int64_t n_clr, uint32_t* __restrict__ clr32, int n_clr32) {
   __shared__ double red[16];
   const int64_t t = blockIdx.x;
   const int64_t fit = blockIdx.y;
+  {
+    const int64_t nb = (int64_t)gridDim.x * gridDim.y, b = fit * gridDim.x + t;
+    for (int64_t e = b * blockDim.x + threadIdx.x; e < n_clr; e += nb * blockDim.x) clr[e] = 0;
+    if (b == 0)
+      for (int e = threadIdx.x; e < n_clr32; e += blockDim.x) clr32[e] = 0u;
+  }
   y += fit * rows;
   kern += fit * rows;
   st += fit * (int64_t)gridDim.x;
@@ -2135,8 +2147,11 @@ __global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
     w.ybar = ybar;
     w.ksum = Sk;
     w.vy = Vy;
+    w.cg = 2.0 / (static_cast<double>(B) * Sk);
     w.step_size = static_cast<float>(static_cast<double>(P.lr) / bc1);
     w.bc2_sqrt = static_cast<float>(sqrt(bc2));
+    w.inv_bc2 = 1.f / w.bc2_sqrt;
+    w.pad = 0.f;
     st[t] = w;
   }
 }
@@ -2481,10 +2496,30 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
 // owning a contiguous slice of mask words (its columns: w, Adam moments, T tables, column bit
 // vectors).  Per Adam step the partial predictions over each slice are exchanged through memory
 // (MI355X_MICROARCH.md inter-workgroup hand-off: 8-byte {value, step tag} granules, stored and
-// polled with sc1) and summed in a fixed order, so every workgroup derives the same g; the gradient and Adam update of a
-// column stay with its owner.  The poll is bounded: a grid that is not co-resident ends (with
-// an error flag) instead of hanging.
+// polled with sc1) and summed in a fixed order, so every workgroup derives the same g; the
+// gradient and Adam update of a column stay with its owner.  The poll is bounded: a grid that is
+// not co-resident ends (with an error flag) instead of hanging.
+//
+// One Adam step = two workgroup barriers.  The step is issue-bound (4 waves share a SIMD), so
+// every phase runs only in the waves that have work in it, all per-thread staging offsets are
+// computed once, and reductions stay inside waves:
+//   B     waves 0..nrb-1, lane = row j: partial p_j over the own words (w nibble tables T, rows
+//         Rb(t)), published at once as a granule
+//   stage every wave: the next step's rows, kernel weights and column bit vectors, and the step
+//         constants (lanes 0..7, vector loads), into registers; the pre-step weights (w_hist)
+//   poll  the B lanes again: the other parts' granules of row j (all loads in flight, then a
+//         bounded spin on the untagged ones), p_j summed over parts 0..P-1 in order (the own
+//         one from the register), g_j, and the 4 entries 4b..4b+3 of the group's 4-bit G table
+//         (b = j & 3; the group's 4 g values by quad DPP moves)
+//   -- barrier 1 --
+//   D     lane = (column, slice of the column's row words): partial (M_b^T g)_i, xor-shuffle
+//         reduction over the slices; the slice-0 lane owns the column: L1/L2 terms and Adam,
+//         then the column quad's 4 T entries (quad DPP moves); staged registers -> LDS
+//         (column vectors double-buffered: D(t) still reads Cb(t) while Cb(t+1) is stored)
+//   -- barrier 2 --
 constexpr uint32_t kMcSpinLimit = 1u << 21;
+constexpr int kMcMaxP = 16;
+constexpr int kMcMaxStage = 4;  // staged words per thread (rows and column vectors each)
 
 __device__ __forceinline__ void st64_sc1(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2492,16 +2527,58 @@ __device__ __forceinline__ void st64_sc1(uint64_t* p, uint64_t v) {
 __device__ __forceinline__ uint64_t ld64_sc1(const uint64_t* p) {
   return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr int kMcMaxP = 8;
 
-template <int CPT>
+// WlmStep from the 12 dwords held by lanes 0..11 of the wave (v_readlane: no LDS, no scalar load)
+constexpr int kStepDw = sizeof(WlmStep) / 4;
+__device__ __forceinline__ WlmStep wlm_step_from_lanes(uint32_t v) {
+  uint32_t d[kStepDw];
+#pragma unroll
+  for (int i = 0; i < kStepDw; ++i) d[i] = __builtin_amdgcn_readlane(v, i);
+  WlmStep s;
+  s.ybar = __hiloint2double(static_cast<int>(d[1]), static_cast<int>(d[0]));
+  s.ksum = __hiloint2double(static_cast<int>(d[3]), static_cast<int>(d[2]));
+  s.vy = __hiloint2double(static_cast<int>(d[5]), static_cast<int>(d[4]));
+  s.cg = __hiloint2double(static_cast<int>(d[7]), static_cast<int>(d[6]));
+  s.step_size = __uint_as_float(d[8]);
+  s.bc2_sqrt = __uint_as_float(d[9]);
+  s.inv_bc2 = __uint_as_float(d[10]);
+  s.pad = 0.f;
+  return s;
+}
+
+// value of lane (lane & ~3) + B of the quad (DPP quad_perm, no LDS)
+template <int B>
+__device__ __forceinline__ float quad_bcast(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), B | (B << 2) | (B << 4) | (B << 6), 0xF, 0xF, false));
+}
+
+// The 4 nibble-table entries vv = 4q..4q+3 (q = lane & 3) of the quad's 4 values x_0..x_3:
+// entry vv = sum of x_b over the set bits b of vv, added in b order (as wlm_build_T / the G
+// build of k_wlm_fit).
+__device__ __forceinline__ void quad_table_entries(float x, float* dst) {
+  const float x0 = quad_bcast<0>(x), x1 = quad_bcast<1>(x), x2 = quad_bcast<2>(x), x3 = quad_bcast<3>(x);
+  const int q = threadIdx.x & 3;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int vv = 4 * q + i;
+    float s = 0.f;
+    s += (vv & 1) ? x0 : 0.f;
+    s += (vv & 2) ? x1 : 0.f;
+    s += (vv & 4) ? x2 : 0.f;
+    s += (vv & 8) ? x3 : 0.f;
+    dst[vv] = s;
+  }
+}
+
+template <int CPL, int STG>
 __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     const uint32_t* __restrict__ bits, const uint32_t* __restrict__ colbits, int64_t rows, int cols, int words,
-    int batch, int bw, int P, int wpp, int n_bs, int n_ds, int64_t n_fits, int xcd_local,
+    int batch, int bw, int P, int wpp, int n_ds, int64_t n_fits, int xcd_local,
     const double* __restrict__ kern,
     const WlmStep* __restrict__ stp, xpg_wlm_params Pm, float* __restrict__ wg, float* __restrict__ mg,
     float* __restrict__ vg, float* __restrict__ p_hist, float* __restrict__ w_hist, uint64_t* xp,
-    uint32_t* err, uint32_t spin_limit, int fault_part) {
+    uint32_t* err, uint32_t spin_limit, int fault_part, uint32_t epoch, int plain_ok) {
+  static_assert(sizeof(WlmStep) == 48, "WlmStep is read as 12 dwords");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int abort_s;  // set by any lane whose poll timed out (or saw the error word): leave the step loop
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2519,10 +2596,10 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
   }
   const int64_t nsteps = (rows + batch - 1) / batch;
   const int w_lo = min(words, part * wpp), w_hi = min(words, w_lo + wpp);
-  const int ow = w_hi - w_lo;                       // own words (0 for surplus parts)
+  const int ow = w_hi - w_lo;                       // own words (>= 1: P = ceil(words / wpp))
   const int c_lo = w_lo * 32, ncol = max(0, min(cols, w_hi * 32) - c_lo);
-  bits += f * rows * words;
-  colbits += f * nsteps * cols * bw;
+  bits += f * rows * words + w_lo;
+  colbits += f * nsteps * cols * bw + (int64_t)c_lo * bw;
   kern += f * rows;
   stp += f * nsteps;
   wg += f * cols + c_lo;
@@ -2530,85 +2607,116 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
   vg += f * cols + c_lo;
   p_hist += f * rows;
   w_hist += f * nsteps * cols + c_lo;
-  xp += f * 2 * P * (int64_t)batch;
+  xp += f * (2 * P * (int64_t)batch + P);  // [2][P][batch] step granules + [P] XCC granules
+  const uint32_t* stp32 = reinterpret_cast<const uint32_t*>(stp);
+  __shared__ int plain_s;
 
-  const int ngrp_alloc = bw * 8;
-  const int ow_max = wpp, ncol_max = wpp * 32;
-  const int rp = ow_max | 1, cp = bw | 1;
-  const int cpad = (ncol_max + 63) & ~63;
-  float* G = reinterpret_cast<float*>(smem);                         // [ngrp_alloc][17]
-  float* bpart = G + ngrp_alloc * kTabPitch;                          // [n_bs][batch]
-  float* dpart = bpart + n_bs * batch;                                // [n_ds][cpad]
-  // dpart is followed by [batch + P * batch] floats no longer used (the exchange is reduced in
-  // registers); kept so the layout matches wlm_layout's byte count
-  const int kb_off = (ngrp_alloc * kTabPitch + n_bs * batch + n_ds * cpad + batch + P * batch + 1) & ~1;
-  double* kbuf = reinterpret_cast<double*>(G + kb_off);              // [batch]
-  float* T = reinterpret_cast<float*>(kbuf + batch);                 // [ow_max*8][17]
-  uint32_t* Rb = reinterpret_cast<uint32_t*>(T + ow_max * 8 * kTabPitch);  // [batch][rp]
-  uint32_t* Cb = Rb + batch * rp;                                     // [ncol_max][cp]
+  const int rp = wpp | 1, cp = bw | 1;
+  const int cbuf = wpp * 32 * cp;                                      // one Cb buffer (words)
+  float* G = reinterpret_cast<float*>(smem);                           // [bw*8][17]
+  const int kb_off = (bw * 8 * kTabPitch + 1) & ~1;
+  double* kbuf = reinterpret_cast<double*>(G + kb_off);                // [batch]
+  float* T = reinterpret_cast<float*>(kbuf + batch);                   // [wpp*8][17]
+  uint32_t* Rb = reinterpret_cast<uint32_t*>(T + wpp * 8 * kTabPitch); // [batch][rp]
+  uint32_t* Cb = Rb + batch * rp;                                      // [2][wpp*32][cp]
 
-  const int nrb = (batch + 63) >> 6, ncb = (ncol + 63) >> 6;
-  const int bsw = (ow + n_bs - 1) / max(n_bs, 1), dsw = (bw + n_ds - 1) / n_ds;
+  const int nrb = (batch + 63) >> 6;
+  const int cw = 64 / n_ds;                       // columns per wave chunk (power of 2, >= 4)
+  const int dsw = (bw + n_ds - 1) / n_ds;         // row words per slice
+  const int col_lo = lane & (cw - 1), sl = lane / cw;
+  const int k0 = sl * dsw, k1 = min(bw, k0 + dsw);
+  const int nchunk = (ow * 32 + cw - 1) / cw;  // chunks over the own words (tail columns: w = 0, zero T entries)
   const float l1s = Pm.l1_lambda / static_cast<float>(cols);
 
-  float w[CPT], m[CPT], v[CPT];
+  // per-thread staging offsets (fixed for the whole fit)
+  int ro[STG], rl[STG], cl[STG];  // rows: global word offset (row * words + word), LDS offset | row << 16
+  const int n_r = batch * ow, n_c = ncol * bw;
 #pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    const int i = tid + c * 1024;
-    w[c] = i < ncol ? wg[i] : 0.f;
-    m[c] = i < ncol ? mg[i] : 0.f;
-    v[c] = i < ncol ? vg[i] : 0.f;
+  for (int q = 0; q < STG; ++q) {
+    const int e = q * 1024 + tid;
+    const int rr = e < n_r ? e / ow : 0, wd = e < n_r ? e - rr * ow : 0;
+    ro[q] = rr * words + wd;
+    rl[q] = (rr * rp + wd) | (rr << 16);
+    const int ce = e < n_c ? e : 0;
+    cl[q] = (ce / bw) * cp + (ce % bw);
   }
-  for (int e = tid; e < ngrp_alloc * kTabPitch; e += 1024) G[e] = 0.f;
-  wlm_build_T<CPT>(w, T, ow * 8);
-
-  uint32_t stg[kStage] = {};  // loaded only where a stage has data; the rest are stored, never read
+  uint32_t sr[STG], sv[STG];
   double kst = 0.0;
-#define XPG_MC_ROWS_LOAD(TT)                                                            \
+#define XPG_MC_LOAD(TT)                                                                 \
   {                                                                                     \
     const int64_t r0_ = (TT) * batch;                                                   \
     const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);      \
-    const int n_ = B_ * ow;                                                             \
-    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+    const uint32_t* rs_ = bits + r0_ * words;                                           \
+    const uint32_t* cs_ = colbits + (TT) * cols * bw;                                   \
+    _Pragma("unroll") for (int q = 0; q < STG; ++q) {                                   \
       const int e_ = q * 1024 + tid;                                                    \
-      if (q * 1024 < n_) {                                                              \
-        const int ee_ = e_ < n_ ? e_ : n_ - 1;                                          \
-        const int rr_ = ee_ / ow;                                                       \
-        stg[q] = bits[(r0_ + rr_) * words + w_lo + (ee_ - rr_ * ow)];                   \
+      if (e_ < n_r) {                                                                   \
+        const int rr_ = rl[q] >> 16;                                                    \
+        sr[q] = rs_[rr_ < B_ ? ro[q] : ro[q] - rr_ * words];                            \
       }                                                                                 \
+      if (e_ < n_c) sv[q] = cs_[e_];                                                    \
     }                                                                                   \
-    kst = kern[r0_ + (tid < B_ ? tid : B_ - 1)];                                        \
+    if (tid < B_) kst = kern[r0_ + tid];                                                \
   }
-#define XPG_MC_ROWS_STORE(TT)                                                           \
+#define XPG_MC_STORE(TT)                                                                \
   {                                                                                     \
-    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
+    uint32_t* cb_ = Cb + ((TT) & 1) * cbuf;                                             \
+    _Pragma("unroll") for (int q = 0; q < STG; ++q) {                                   \
       const int e_ = q * 1024 + tid;                                                    \
-      if (e_ < batch * ow) Rb[(e_ / ow) * rp + (e_ % ow)] = stg[q];                     \
+      if (e_ < n_r) Rb[rl[q] & 0xFFFF] = sr[q];                                         \
+      if (e_ < n_c) cb_[cl[q]] = sv[q];                                                 \
     }                                                                                   \
-    const int64_t r0_ = (TT) * batch;                                                   \
-    const int B_ = static_cast<int>((rows - r0_) < batch ? (rows - r0_) : batch);      \
     if (tid < batch) kbuf[tid] = kst;                                                   \
-    for (int e_ = tid + 1024; e_ < B_; e_ += 1024) kbuf[e_] = kern[r0_ + e_];           \
   }
-#define XPG_MC_COLS_LOAD(TT)                                                            \
-  {                                                                                     \
-    const uint32_t* src_ = colbits + ((TT) * cols + c_lo) * bw;                         \
-    const int n_ = ncol * bw;                                                           \
-    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
-      const int e_ = q * 1024 + tid;                                                    \
-      if (q * 1024 < n_) stg[q] = src_[e_ < n_ ? e_ : n_ - 1];                          \
-    }                                                                                   \
+
+  // own columns: column chunk (wave + 16 c), lane col_lo; the slice-0 lane holds w, m, v
+  float w[CPL], m[CPL], v[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int i = (wave + 16 * c) * cw + col_lo;
+    const bool own = sl == 0 && i < ncol;
+    w[c] = own ? wg[i] : 0.f;
+    m[c] = own ? mg[i] : 0.f;
+    v[c] = own ? vg[i] : 0.f;
   }
-#define XPG_MC_COLS_STORE()                                                             \
-  {                                                                                     \
-    _Pragma("unroll") for (int q = 0; q < kStage; ++q) {                                \
-      const int e_ = q * 1024 + tid;                                                    \
-      if (e_ < ncol * bw) Cb[(e_ / bw) * cp + (e_ % bw)] = stg[q];                      \
-    }                                                                                   \
+  for (int e = tid; e < bw * 8 * kTabPitch; e += 1024) G[e] = 0.f;
+  // initial T: quads of own columns (tail columns hold w = 0, so tail entries are 0)
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = wave + 16 * c;
+    if (ch < nchunk && sl == 0) {
+      const int i = ch * cw + col_lo;
+      if (i < ow * 32) quad_table_entries(w[c], T + (i >> 2) * kTabPitch);
+    }
   }
-  XPG_MC_ROWS_LOAD(0)
-  XPG_MC_ROWS_STORE(0)
+  XPG_MC_LOAD(0)
+  uint32_t stw = lane < kStepDw ? stp32[lane] : 0u;
+  // XCC handshake (once per fit): when every part of the fit runs on one XCD, the step granules
+  // are published with workgroup-scope stores, which keep the line in that XCD's L2, so the
+  // parts' sc1 polls are served from L2 instead of memory (speed only: the test is made at run
+  // time, so any placement stays correct).  Tag epoch << 16 (step 0).
+  if (wave == 0) {
+    uint64_t* xc = xp + 2 * P * (int64_t)batch;
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu;  // HW_REG_XCC_ID[3:0]
+    const uint32_t htag = epoch << 16;
+    if (lane == 0) st64_sc1(xc + part, (static_cast<uint64_t>(htag) << 32) | xcc);
+    bool same = true;
+    if (lane < P && plain_ok) {
+      uint64_t gx = ld64_sc1(xc + lane);
+      uint32_t n = 0;
+      while (static_cast<uint32_t>(gx >> 32) != htag && n <= spin_limit) {
+        __builtin_amdgcn_s_sleep(1);
+        gx = ld64_sc1(xc + lane);
+        ++n;
+      }
+      same = static_cast<uint32_t>(gx >> 32) == htag && static_cast<uint32_t>(gx) == xcc;
+    }
+    const bool all = __ballot(!same) == 0ull && plain_ok;
+    if (lane == 0) plain_s = all ? 1 : 0;
+  }
+  XPG_MC_STORE(0)
   lds_barrier();
+  const bool plain = plain_s != 0;
 #ifdef XPG_WLM_STAMPS
   uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t stamp_last = __builtin_amdgcn_s_memtime();
@@ -2617,179 +2725,154 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
   for (int64_t t = 0; t < nsteps; ++t) {
     const int64_t r0 = t * batch;
     const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
-    const WlmStep sc = stp[t];
-    XPG_MC_COLS_LOAD(t)
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      const int i = tid + c * 1024;
-      if (i < ncol) w_hist[t * cols + i] = w[c];
-    }
-    // ---- B: partial predictions over the own words (lanes = rows)
-    for (int it = wave; it < nrb * n_bs; it += 16) {
-      const int rb = it % nrb, sl = it / nrb;
-      const int j = rb * 64 + lane;
-      const int wd0 = sl * bsw, wd1 = min(ow, wd0 + bsw);
-      float s = 0.f;
+    const WlmStep sc = wlm_step_from_lanes(stw);
+    uint64_t* xs = xp + (t & 1) * P * (int64_t)batch;
+    const uint32_t tag = (epoch << 16) | static_cast<uint32_t>(t + 1);
+    const int j = wave * 64 + lane;  // B / poll row
+    const bool prow = wave < nrb && j < B;
+    // ---- B: partial p_j over the own words, published from the lane
+    float pown = 0.f;
+    if (wave < nrb) {
       if (j < B) {
         const uint32_t* row = Rb + j * rp;
-        for (int k0 = wd0; k0 < wd1; k0 += 2) {
+        for (int kw = 0; kw < ow; kw += 2) {  // 16 lookups in flight (lgkmcnt limit 15)
           uint32_t wv[2];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int wd = k0 + h;
-            wv[h] = row[wd < wd1 ? wd : wd0];
-          }
+          for (int h = 0; h < 2; ++h) wv[h] = row[kw + h < ow ? kw + h : kw];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const int wd = k0 + h;
-            const float x = nib8(T + ((wd < wd1 ? wd : wd0) * 8) * kTabPitch, wv[h]);
-            s += wd < wd1 ? x : 0.f;
+            const float x = nib8(T + ((kw + h < ow ? kw + h : kw) * 8) * kTabPitch, wv[h]);
+            pown += kw + h < ow ? x : 0.f;
+          }
+        }
+        const bool skip_pub = fault_part == part && f == 0 && t == 0;  // fault injection (tests only)
+        if (!skip_pub) {
+          const uint64_t gv = (static_cast<uint64_t>(tag) << 32) | __float_as_uint(pown);
+          if (plain)
+            __hip_atomic_store(xs + part * (int64_t)batch + j, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          else
+            st64_sc1(xs + part * (int64_t)batch + j, gv);
+        }
+      }
+    }
+    XPG_STAMP(0)
+    // ---- stage: the next step's data and constants; the pre-step weights
+    if (t + 1 < nsteps) {
+      XPG_MC_LOAD(t + 1)
+      stw = lane < kStepDw ? stp32[(t + 1) * kStepDw + lane] : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int i = (wave + 16 * c) * cw + col_lo;
+      if (sl == 0 && i < ncol) w_hist[t * cols + i] = w[c];
+    }
+    XPG_STAMP(1)
+    // ---- poll: p_j over the parts in order, g_j, the G table entries
+    if (wave < nrb) {
+      float p = 0.f;
+      if (prow) {
+        uint64_t gr[kMcMaxP];
+#pragma unroll
+        for (int q = 0; q < kMcMaxP; ++q)
+          gr[q] = q < P && q != part ? ld64_sc1(xs + q * (int64_t)batch + j) : (static_cast<uint64_t>(tag) << 32);
+#pragma unroll
+        for (int q = 0; q < kMcMaxP; ++q) {
+          if (q < P) {
+            uint32_t n = 0;
+            while (static_cast<uint32_t>(gr[q] >> 32) != tag) {
+              __builtin_amdgcn_s_sleep(1);
+              gr[q] = ld64_sc1(xs + q * (int64_t)batch + j);
+              ++n;
+              // bounded: a partner that never publishes (grid not co-resident, or a partner
+              // that already left after an error) ends the fit with the error word set, which
+              // xpg_wlm_fit hands to the caller's status word
+              if (n > spin_limit || ((n & 63u) == 0 &&
+                                     __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                abort_s = 1;
+                break;
+              }
+            }
+            p += q == part ? pown : __uint_as_float(static_cast<uint32_t>(gr[q]));
           }
         }
       }
-      if (j < batch) bpart[sl * batch + j] = s;
+      float g = 0.f;
+      if (prow) {
+        if (part == 0) p_hist[r0 + j] = p;
+        g = static_cast<float>(kbuf[j] * sc.cg * (static_cast<double>(p) - sc.ybar));
+      }
+      // rows >= B of the last group hold g = 0; whole quads stay inside the batch
+      if (j < ((B + 3) & ~3)) quad_table_entries(g, G + (j >> 2) * kTabPitch);
     }
-    XPG_STAMP(0)
-    lds_barrier();
-    XPG_STAMP(1)
-    // ---- exchange: publish this slice's partial p_j as 8-byte {value, step tag} granules
-    // (write-through sc1 stores; parity double-buffered), then poll every slice's granule of
-    // row j until it carries this step's tag
-    uint64_t* xs = xp + (t & 1) * P * (int64_t)batch;
-    const uint32_t tag = static_cast<uint32_t>(t + 1);
-    const bool skip_pub = fault_part == part && f == 0 && t == 0;  // fault injection (tests only)
-    for (int j = tid; j < B && !skip_pub; j += 1024) {
-      float p = 0.f;
-      for (int sl = 0; sl < n_bs; ++sl) p += bpart[sl * batch + j];
-      st64_sc1(xs + part * (int64_t)batch + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(p));
-    }
-    XPG_MC_COLS_STORE()
     XPG_STAMP(2)
+    lds_barrier();  // G complete; Rb(t), kbuf(t) free
     XPG_STAMP(3)
-    // ---- poll, g and the G tables in one phase, within 16-lane groups (no barrier between):
-    // lane (grp, vv) owns table entry G[grp][vv]; its row is j = 4 grp + (vv & 3) and it polls
-    // slices q = vv >> 2 and q + 4 of that row (P <= 8); two xor-shuffles sum the 4 lanes of a
-    // row (the same tree in every workgroup, so every workgroup derives the same g), and the
-    // entry adds the g of its group's rows selected by the bits of vv (row order 0..3).
+    if (abort_s) break;  // workgroup-uniform (read after the barrier): the fit is invalid, stop
+    // ---- D + Adam + T on the own column chunks
     {
-      const int ngrp = (B + 3) >> 2;
-      const double cg = 2.0 / (static_cast<double>(B) * sc.ksum);
-      for (int e = tid; e < ngrp * 16; e += 1024) {  // whole 16-lane groups per iteration
-        const int grp = e >> 4, vv = e & 15, b = vv & 3, qq = vv >> 2;
-        const int j = 4 * grp + b;
-        float s = 0.f;
-        if (j < B) {
+      const uint32_t* cbt = Cb + (t & 1) * cbuf;
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int q = qq + 4 * h;
-            if (q < P) {
-              const uint64_t* src = xs + q * (int64_t)batch + j;
-              uint64_t gr = ld64_sc1(src);
-              uint32_t n = 0;
-              while (static_cast<uint32_t>(gr >> 32) != tag) {
-                __builtin_amdgcn_s_sleep(1);
-                gr = ld64_sc1(src);
-                ++n;
-                // bounded: a partner that never publishes (grid not co-resident, or a partner
-                // that already left after an error) ends the fit with the error word set, which
-                // xpg_wlm_fit hands to the caller's status word
-                if (n > spin_limit || ((n & 63u) == 0 &&
-                                       __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                  __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  abort_s = 1;
-                  break;
-                }
+      for (int c = 0; c < CPL; ++c) {
+        const int ch = wave + 16 * c;
+        if (ch < nchunk) {  // wave-uniform
+          const int i = ch * cw + col_lo;
+          float s = 0.f;
+          if (i < ncol) {
+            const uint32_t* cb = cbt + i * cp;
+            for (int kk = k0; kk < k1; kk += 2) {
+              uint32_t wv[2];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) wv[h] = cb[kk + h < k1 ? kk + h : kk];
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const float x = nib8(G + ((kk + h < k1 ? kk + h : kk) * 8) * kTabPitch, wv[h]);
+                s += kk + h < k1 ? x : 0.f;
               }
-              s += __uint_as_float(static_cast<uint32_t>(gr));
             }
           }
+          for (int o = cw; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+          if (sl == 0) {
+            if (i < ncol) {
+              const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
+              float gi = fmaf(l1s, sg, s);
+              gi = fmaf(Pm.weight_decay, w[c], gi);
+              m[c] = fmaf(1.f - Pm.beta1, gi - m[c], m[c]);
+              v[c] = fmaf(1.f - Pm.beta2, gi * gi, v[c] * Pm.beta2);
+              // v_sqrt / v_rcp (1 ulp) instead of the correctly rounded sequences: the Adam update
+              // is the step's dependent tail (torch: (sqrt(v) / bc2_sqrt + eps), addcdiv)
+              const float denom = __builtin_amdgcn_sqrtf(v[c]) * sc.inv_bc2 + Pm.eps;
+              w[c] = w[c] - sc.step_size * (m[c] * __builtin_amdgcn_rcpf(denom));
+            }
+            if (i < ow * 32) quad_table_entries(w[c], T + (i >> 2) * kTabPitch);
+          }
         }
-        s += __shfl_xor(s, 4, 16);
-        s += __shfl_xor(s, 8, 16);
-        float g = 0.f;
-        if (j < B) {
-          if (part == 0 && qq == 0) p_hist[r0 + j] = s;
-          g = static_cast<float>(kbuf[j] * cg * (static_cast<double>(s) - sc.ybar));
-        }
-        float acc = 0.f;
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
-          const float gb = __shfl(g, bb, 16);
-          acc += ((vv >> bb) & 1) ? gb : 0.f;
-        }
-        G[grp * kTabPitch + vv] = acc;
       }
     }
     XPG_STAMP(4)
-    lds_barrier();  // G and Cb(t) complete; Rb, kbuf free
+    if (t + 1 < nsteps) XPG_MC_STORE(t + 1)
     XPG_STAMP(5)
-    if (abort_s) break;  // workgroup-uniform (read after the barrier): the fit is invalid, stop
-    if (t + 1 < nsteps) XPG_MC_ROWS_LOAD(t + 1)
-    // ---- D: gradient of the own columns (lanes = columns)
-    for (int it = wave; it < ncb * n_ds; it += 16) {
-      const int cbk = it % ncb, sl = it / ncb;
-      const int i = cbk * 64 + lane;
-      const int k0 = sl * dsw, k1 = min(bw, k0 + dsw);
-      float s = 0.f;
-      if (i < ncol) {
-        const uint32_t* cb = Cb + i * cp;
-        for (int kk = k0; kk < k1; kk += 2) {
-          uint32_t wv[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int k = kk + h;
-            wv[h] = cb[k < k1 ? k : k0];
-          }
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int k = kk + h;
-            const float x = nib8(G + ((k < k1 ? k : k0) * 8) * kTabPitch, wv[h]);
-            s += k < k1 ? x : 0.f;
-          }
-        }
-      }
-      if (i < cpad) dpart[sl * cpad + i] = s;
-    }
-    lds_barrier();
+    lds_barrier();  // T, Rb(t+1), kbuf(t+1), Cb(t+1) complete
     XPG_STAMP(6)
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      const int i = tid + c * 1024;
-      if (i < ncol) {
-        float s = 0.f;
-        for (int sl = 0; sl < n_ds; ++sl) s += dpart[sl * cpad + i];
-        const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
-        float g = fmaf(l1s, sg, s);
-        g = fmaf(Pm.weight_decay, w[c], g);
-        m[c] = fmaf(1.f - Pm.beta1, g - m[c], m[c]);
-        v[c] = fmaf(1.f - Pm.beta2, g * g, v[c] * Pm.beta2);
-        const float denom = sqrtf(v[c]) / sc.bc2_sqrt + Pm.eps;
-        w[c] = w[c] - sc.step_size * (m[c] / denom);
-      }
-    }
-    wlm_build_T<CPT>(w, T, ow * 8);
-    if (t + 1 < nsteps) XPG_MC_ROWS_STORE(t + 1)
-    lds_barrier();
     XPG_STAMP(7)
   }
 #ifdef XPG_WLM_STAMPS
+  stamp_acc[7] = plain ? nsteps : 0;  // reported as 1 per step: the L2-resident publish path ran
   if (blockIdx.x == 0 && (tid == 0 || tid == 1023)) {
     for (int k = 0; k < 8; ++k) g_wlm_stamps[tid == 0 ? 0 : 1][k] = stamp_acc[k];
   }
 #endif
 #pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    const int i = tid + c * 1024;
-    if (i < ncol) {
+  for (int c = 0; c < CPL; ++c) {
+    const int i = (wave + 16 * c) * cw + col_lo;
+    if (sl == 0 && i < ncol) {
       wg[i] = w[c];
       mg[i] = m[c];
       vg[i] = v[c];
     }
   }
-#undef XPG_MC_ROWS_LOAD
-#undef XPG_MC_ROWS_STORE
-#undef XPG_MC_COLS_LOAD
-#undef XPG_MC_COLS_STORE
+#undef XPG_MC_LOAD
+#undef XPG_MC_STORE
 }
 
 
@@ -3090,8 +3173,11 @@ __global__ __launch_bounds__(64) void k_gw_loss(const double* __restrict__ tk_pa
 }
 
 
-__global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t* __restrict__ out) {
+// Also hands the fit's status word to the caller: the multi-workgroup exchange's error word, or 0.
+__global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t* __restrict__ out,
+                               const uint32_t* __restrict__ errw, int32_t* __restrict__ status) {
   if (threadIdx.x != 0) return;
+  if (status && blockIdx.x == 0) *status = errw ? static_cast<int32_t>(*errw) : 0;
   v += blockIdx.x * n;
   out += blockIdx.x;
   double best = INFINITY;
@@ -3937,7 +4023,7 @@ struct WlmWs {
   size_t lds;
   // multi-workgroup fit
   bool mc, xcd;
-  int P, wpp, mc_bs, mc_ds;
+  int P, wpp, mc_ds, mc_cpl, mc_stg;
   size_t xp_off, cnt_off, lds_mc;
   // grid (many-column) fit
   bool grid;
@@ -4023,28 +4109,48 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   L->lds = g_bytes() + (L->stage ? t_bytes + stage_bytes : 0);
   // multi-workgroup fit: P workgroups (one per CU, all co-resident) per fit
   L->mc = false;
-  if (!wlm_env("single") && (words >= 8 || wlm_env("mc"))) {
+  if (!wlm_env("single") && (words >= 8 || wlm_env("mc")) && batch <= 1024) {
     const char* xe = getenv("XPG_MC_XCD");
     L->xcd = !(xe && std::strcmp(xe, "0") == 0);
-    int P = std::min(kMcMaxP, std::max(2, words / 4));
+    const char* pe = getenv("XPG_MC_P");  // tuning override of the parts per fit
+    int P = std::min(kMcMaxP, std::max(2, pe ? atoi(pe) : static_cast<int>(cdiv(words, 3))));
+    // the staged rows / column vectors must fit kMcMaxStage words per thread: more parts if not
+    while (P < kMcMaxP && std::max<int64_t>(batch, 32 * L->bw) * cdiv(words, P) > kMcMaxStage * 1024) ++P;
     while (P > 1 && (L->xcd ? cdiv(n_fits, 8) * P > device_cus() / 8 : n_fits * P > device_cus())) --P;
     if (P >= 2) {
       const int wpp = static_cast<int>(cdiv(words, P));
       P = static_cast<int>(cdiv(words, wpp));
-      const int bs = wlm_slices(cdiv(batch, 64), wpp);
-      const int ds = wlm_slices(cdiv((int64_t)wpp * 32, 64), L->bw);
-      const int64_t cpad = ((int64_t)wpp * 32 + 63) & ~int64_t(63);
-      const size_t fl = sizeof(float) *
-                        (size_t)((L->bw * 8 * kTabPitch + bs * batch + ds * cpad + batch + P * batch + 1) & ~int64_t(1));
-      const size_t lds = fl + sizeof(double) * (size_t)batch + sizeof(float) * (size_t)wpp * 8 * kTabPitch +
-                         sizeof(uint32_t) * ((size_t)batch * (wpp | 1) + (size_t)wpp * 32 * (L->bw | 1));
-      if (P >= 2 && lds <= lds_cap && (int64_t)batch * wpp <= kStage * 1024 &&
-          (int64_t)wpp * 32 * L->bw <= kStage * 1024) {
+      // slices of the column row words per D lane.  A SIMD issues the waves of ceil(chunks / 4)
+      // chunks, each ~4 instructions per lookup plus ~100 for Adam, the T quad and the loop, plus
+      // the xor reduction; each lane's lookups also wait one LDS round trip (~400 cycles) per 16
+      // in flight (probe-measured on the c2 fit); at most 4 column chunks per wave
+      int nd_best = 0, cpl_best = 0;
+      int64_t cost_best = INT64_MAX;
+      const char* de = getenv("XPG_MC_DS");  // tuning override
+      for (int nd = 1, lg = 0; nd <= 16; nd <<= 1, ++lg) {
+        const int64_t chunks = cdiv((int64_t)wpp * 32, 64 / nd), cpl = cdiv(chunks, 16);
+        if (cpl > 4 || (de && atoi(de) != nd)) continue;
+        const int64_t look = cdiv(L->bw, nd) * 8;
+        const int64_t cost = cdiv(chunks, 4) * (look * 4 + 100 + 10 * lg) + cdiv(look, 16) * 400;
+        if (cost < cost_best) {
+          cost_best = cost;
+          nd_best = nd;
+          cpl_best = static_cast<int>(cpl == 3 ? 4 : cpl);
+        }
+      }
+      const int64_t stage = std::max<int64_t>(batch * wpp, (int64_t)wpp * 32 * L->bw);
+      int stg = static_cast<int>(cdiv(stage, 1024));
+      stg = stg <= 1 ? 1 : stg <= 2 ? 2 : 4;
+      const size_t lds = sizeof(float) * (size_t)((L->bw * 8 * kTabPitch + 1) & ~int64_t(1)) +
+                         sizeof(double) * (size_t)batch + sizeof(float) * (size_t)wpp * 8 * kTabPitch +
+                         sizeof(uint32_t) * ((size_t)batch * (wpp | 1) + 2 * (size_t)wpp * 32 * (L->bw | 1));
+      if (nd_best > 0 && lds <= lds_cap && stage <= kMcMaxStage * 1024) {
         L->mc = true;
         L->P = P;
         L->wpp = wpp;
-        L->mc_bs = bs;
-        L->mc_ds = ds;
+        L->mc_ds = nd_best;
+        L->mc_cpl = cpl_best;
+        L->mc_stg = stg;
         L->lds_mc = std::max<size_t>(lds, 81 * 1024);  // > half the CU's LDS: one workgroup per CU
       }
     }
@@ -4062,7 +4168,7 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   L->tglob_off = off;
   off += align_up(L->stage ? 0 : F * t_bytes);
   L->xp_off = off;
-  off += align_up(L->mc ? F * sizeof(uint64_t) * 2 * L->P * (size_t)batch : 0);
+  off += align_up(L->mc ? F * sizeof(uint64_t) * (2 * L->P * (size_t)batch + L->P) : 0);
   L->cnt_off = off;
   off += align_up(sizeof(uint32_t) * (F + 1));
   L->total = off;
@@ -4071,7 +4177,7 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
 
 static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                         const float* y, const double* kernel, const xpg_wlm_params& P, int64_t step0, float* w,
-                        float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, char* ws,
+                        float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, int32_t* status, char* ws,
                         const WlmWs& L, hipStream_t st) {
   const int64_t steps = cdiv(rows, batch);
   const int64_t words = cdiv(cols, 32);
@@ -4084,7 +4190,7 @@ static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   double* tk_part = reinterpret_cast<double*>(ws + L.tk_off);
   double* aw_part = reinterpret_cast<double*>(ws + L.aw_off);
   hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib, P,
-                     step0, stp);
+                     step0, stp, nullptr, int64_t(0), nullptr, 0);
   XPG_LAUNCHED();
   XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gw_grad),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_g)));
@@ -4102,7 +4208,7 @@ static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   hipLaunchKernelGGL(k_gw_loss, dim3(static_cast<unsigned>(steps), nf), dim3(64), 0, st, tk_part, L.n_tk, aw_part,
                      L.n_wg, stp, rows, cols, ib, P.l1_lambda, losses);
   XPG_LAUNCHED();
-  hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch);
+  hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch, nullptr, status);
   XPG_LAUNCHED();
   return XPG_OK;
 }
@@ -4121,6 +4227,7 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
                 int32_t* status, void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
   XPG_REQ(params != nullptr, "wlm_fit: params required");
   XPG_REQ(n_fits <= 65535, "wlm_fit: at most 65535 fits per launch");
+  XPG_REQ(rows / std::max<int64_t>(batch, 1) < 65535, "wlm_fit: at most 65534 steps per fit");
   WlmWs L;
   int rc = wlm_layout(n_fits, rows, cols, batch, &L);
   if (rc) return rc;
@@ -4128,9 +4235,8 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   hipStream_t st = S(stream);
   char* ws = static_cast<char*>(workspace);
   WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
-  if (status) XPG_HIP(hipMemsetAsync(status, 0, sizeof(int32_t), st));
   if (L.grid) return wlm_fit_grid(n_fits, bits, rows, cols, batch, y, kernel, *params, step0, w, adam_m, adam_v,
-                                  losses, best_epoch, ws, L, st);
+                                  losses, best_epoch, status, ws, L, st);
   uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
   float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
   float* w_hist = reinterpret_cast<float*>(ws + L.whist_off);
@@ -4139,42 +4245,51 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   const int words = words_of(cols);
   const int ic = static_cast<int>(cols), ib = static_cast<int>(batch);
   const unsigned nf = static_cast<unsigned>(n_fits);
+  // the multi-workgroup fit's exchange slots and error words are cleared by k_wlm_stats
+  const int64_t n_xp = L.mc ? n_fits * (2 * L.P * batch + L.P) : 0;
   hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib,
-                     *params, step0, stp);
+                     *params, step0, stp, L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
+                     L.mc ? reinterpret_cast<uint32_t*>(ws + L.cnt_off) : nullptr, L.mc ? static_cast<int>(n_fits + 1) : 0);
   XPG_LAUNCHED();
   const int64_t waves = steps * words * cdiv(batch, 64);
   hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(waves, 4)), nf), dim3(256), 0, st, bits, rows,
                      ic, words, ib, L.bw, steps, colbits);
   XPG_LAUNCHED();
   bool launched = false;
+  const uint32_t* errw = nullptr;
   if (L.mc) {
     uint32_t* cnt = reinterpret_cast<uint32_t*>(ws + L.cnt_off);
     uint64_t* xp = reinterpret_cast<uint64_t*>(ws + L.xp_off);
-    // granule tags restart at 1 every call: clear the exchange slots and the error word
-    XPG_HIP(hipMemsetAsync(xp, 0, sizeof(uint64_t) * 2 * L.P * (size_t)batch * n_fits, st));
-    XPG_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (n_fits + 1), st));
-    const int cpt_mc = static_cast<int>(cdiv((int64_t)L.wpp * 32, 1024));
+    // granule tags carry a per-call epoch (stale cache lines of earlier calls never match)
+    static uint32_t epoch = 0;
+    epoch = (epoch + 1) & 0xFFFFu;
+    if (epoch == 0) epoch = 1;
+    const char* pl = getenv("XPG_MC_PLAIN");  // 0: sc1 publish stores even when a fit sits on one XCD
+    const int plain_ok = pl && std::strcmp(pl, "0") == 0 ? 0 : 1;
     // test hooks: XPG_MC_SPIN (poll bound), XPG_MC_FAULT (part of fit 0 that skips its first publish)
     const char* se = getenv("XPG_MC_SPIN");
     const char* fe = getenv("XPG_MC_FAULT");
     const uint32_t spin = se ? static_cast<uint32_t>(strtoul(se, nullptr, 10)) : kMcSpinLimit;
     const int fault = fe ? atoi(fe) : -1;
     const dim3 grid(static_cast<unsigned>(L.xcd ? 8 * L.P * cdiv(n_fits, 8) : n_fits * L.P));
-#define XPG_WLM_MC(C)                                                                                       \
-    if (!launched && cpt_mc <= C) {                                                                         \
-      XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit_mc<C>),                          \
+#define XPG_WLM_MC(C, G)                                                                                    \
+    if (!launched && L.mc_cpl == C && L.mc_stg == G) {                                                      \
+      XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit_mc<C, G>),                       \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_mc))); \
-      hipLaunchKernelGGL(k_wlm_fit_mc<C>, grid, dim3(1024), L.lds_mc, st, bits, colbits, rows, ic, words, ib, L.bw, \
-                         L.P, L.wpp, L.mc_bs, L.mc_ds, n_fits, L.xcd ? 1 : 0, kernel, stp, *params, w, adam_m,    \
-                         adam_v, p_hist, w_hist, xp, cnt + n_fits, spin, fault);                           \
+      hipLaunchKernelGGL((k_wlm_fit_mc<C, G>), grid, dim3(1024), L.lds_mc, st, bits, colbits, rows, ic, words, ib, \
+                         L.bw, L.P, L.wpp, L.mc_ds, n_fits, L.xcd ? 1 : 0, kernel, stp, *params, w, adam_m,      \
+                         adam_v, p_hist, w_hist, xp, cnt + n_fits, spin, fault, epoch, plain_ok);            \
       XPG_LAUNCHED();                                                                                       \
       launched = true;                                                                                      \
     }
-    XPG_WLM_MC(1) XPG_WLM_MC(2) XPG_WLM_MC(4)
+    XPG_WLM_MC(1, 1) XPG_WLM_MC(1, 2) XPG_WLM_MC(1, 4)
+    XPG_WLM_MC(2, 1) XPG_WLM_MC(2, 2) XPG_WLM_MC(2, 4)
+    XPG_WLM_MC(4, 1) XPG_WLM_MC(4, 2) XPG_WLM_MC(4, 4)
 #undef XPG_WLM_MC
     if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported slice width");
     // the exchange's error word (nonzero: a partner's poll timed out, the weights are invalid)
-    if (status) XPG_HIP(hipMemcpyAsync(status, cnt + n_fits, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    // reaches the caller's status through k_argmin_first
+    errw = cnt + n_fits;
   }
   const int cpt = static_cast<int>(cdiv(cols, 1024));
 #define XPG_WLM(C, TL)                                                                                     \
@@ -4194,7 +4309,7 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   hipLaunchKernelGGL(k_wlm_loss, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, p_hist, w_hist, kernel,
                      stp, rows, ic, ib, params->l1_lambda, losses);
   XPG_LAUNCHED();
-  hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch);
+  hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch, errw, status);
   XPG_LAUNCHED();
   return XPG_OK;
 }

@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
            (long)batch, ms * 1e3, ms * 1e3 / steps);
     const bool mc = getenv("XPG_WLM") == nullptr || strcmp(getenv("XPG_WLM"), "single") != 0;
     const char* nm1[8] = {"B lookups", "syncA", "G + COLS_ST", "sync1", "D lookups", "syncD", "Adam+T+ROWS", "sync2"};
-    const char* nm2[8] = {"B lookups", "syncA", "publish+COLS", "bar+signal+poll", "p sum + g", "G build+bar", "D + bar", "Adam+T+ROWS+bar"};
+    const char* nm2[8] = {"B+publish", "stage issue", "poll+g+G", "bar1", "D+Adam+T", "stage store", "bar2", "plain path"};
     const char* const* nm = mc ? nm2 : nm1;
     for (int q = 0; q < 8; ++q) printf("  %-12s wave0 %8.0f  last %8.0f\n", nm[q], (double)st[0][q] / steps, (double)st[1][q] / steps);
   }
