@@ -2157,34 +2157,33 @@ __global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
 }
 
 // colbits[(t * cols + c) * bw + jw] bit b = mask bit (row t*batch + 32*jw + b, column c)
+// Lane = (step t, 32-row block jw, mask word wd), wd fastest: 32 row words read coalesced across
+// the lanes of a block, one in-register 32 x 32 bit transpose, 32 column words stored.
 __global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict__ bits, int64_t rows,
                                                      int cols, int words, int batch, int bw,
                                                      int64_t steps, uint32_t* __restrict__ colbits) {
-  const int lane = threadIdx.x & 63;
-  const int chunks = (batch + 63) / 64;
-  int64_t wave = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int64_t per_fit = steps * words * chunks;
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t fit = blockIdx.y;
-  if (wave >= per_fit) return;  // wave-uniform exit
+  if (gid >= steps * bw * words) return;
   bits += fit * rows * words;
   colbits += fit * steps * cols * bw;
-  const int64_t t = wave / ((int64_t)words * chunks);
-  const int rem = static_cast<int>(wave - t * words * chunks);
-  const int wd = rem / chunks, ch = rem - wd * chunks;
+  const int wd = static_cast<int>(gid % words);
+  const int64_t tk = gid / words;
+  const int jw = static_cast<int>(tk % bw);
+  const int64_t t = tk / bw;
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
-  const int j = ch * 64 + lane;
-  const uint32_t word = j < B ? bits[(r0 + j) * words + wd] : 0u;
-#pragma unroll 4
-  for (int c = 0; c < 32; ++c) {
-    const unsigned long long m = __ballot((word >> c) & 1u);
-    const int col = wd * 32 + c;
-    if (lane == c && col < cols) {
-      uint32_t* dst = colbits + ((int64_t)t * cols + col) * bw + 2 * ch;
-      dst[0] = static_cast<uint32_t>(m);
-      if (2 * ch + 1 < bw) dst[1] = static_cast<uint32_t>(m >> 32);
-    }
+  uint32_t x[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int j = 32 * jw + i;
+    x[i] = j < B ? bits[(r0 + j) * words + wd] : 0u;
   }
+  transpose32(x);
+  uint32_t* dst = colbits + ((int64_t)t * cols + (int64_t)wd * 32) * bw + jw;
+#pragma unroll
+  for (int b = 0; b < 32; ++b)
+    if (wd * 32 + b < cols) dst[(int64_t)b * bw] = x[b];
 }
 
 
@@ -4251,9 +4250,9 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
                      *params, step0, stp, L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
                      L.mc ? reinterpret_cast<uint32_t*>(ws + L.cnt_off) : nullptr, L.mc ? static_cast<int>(n_fits + 1) : 0);
   XPG_LAUNCHED();
-  const int64_t waves = steps * words * cdiv(batch, 64);
-  hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(waves, 4)), nf), dim3(256), 0, st, bits, rows,
-                     ic, words, ib, L.bw, steps, colbits);
+  const int64_t lanes = steps * L.bw * words;
+  hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(lanes, 256)), nf), dim3(256), 0, st, bits, rows, ic,
+                     words, ib, L.bw, steps, colbits);
   XPG_LAUNCHED();
   bool launched = false;
   const uint32_t* errw = nullptr;
