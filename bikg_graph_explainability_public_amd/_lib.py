@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -39,7 +39,8 @@ class LayerDesc(ctypes.Structure):
                 ("tgt_f0", c_vp),
                 ("agg_ptr", c_vp), ("agg_src", c_vp), ("agg_f0", c_vp), ("self_mult", c_vp),
                 ("terms", TermDesc * MAX_TERMS), ("weight", c_vp), ("bias", c_vp),
-                ("tgt_type", c_vp), ("n_types", c_i32)]
+                ("tgt_type", c_vp), ("n_types", c_i32),
+                ("agg_eid", c_vp), ("self_ptr", c_vp), ("self_eid", c_vp)]
 
 
 class HeadDesc(ctypes.Structure):
@@ -51,7 +52,9 @@ class ForwardPlanDesc(ctypes.Structure):
     _fields_ = [("cols", c_i64), ("n_rel", c_i32), ("n0", c_i32), ("f0_node", c_vp),
                 ("deg_ptr", c_vp), ("deg_src", c_vp), ("n_deg_edges", c_i64), ("n_layers", c_i32),
                 ("layers", ctypes.POINTER(LayerDesc)), ("n_head", c_i32),
-                ("head", ctypes.POINTER(HeadDesc)), ("out_col", c_i32)]
+                ("head", ctypes.POINTER(HeadDesc)), ("out_col", c_i32),
+                ("edge_masks", c_i32), ("deg_eid", c_vp), ("edge_dot", c_i32), ("dot_a", c_i32),
+                ("dot_b", c_i32), ("dot_act", c_i32)]
 
 
 class WlmParams(ctypes.Structure):

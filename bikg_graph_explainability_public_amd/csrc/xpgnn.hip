@@ -526,10 +526,12 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
 // kin[(b * n_rel + r) * n0 + p] = kept in-degree of F_0 node p under relation r for mask row b
 // (self-loops excluded), or -1 when the node itself is masked out (then it keeps only the
 // GCN self-loop / an empty SAGE neighbourhood).
+// Edge masks (deg_eid != NULL, Data.perturb_edge): every node is active and an in-edge counts iff
+// its own column bit is set.
 __global__ void k_degree(const uint32_t* __restrict__ bits, int64_t rows, int words, int n0,
                          int n_rel, const int32_t* __restrict__ f0_node,
                          const int32_t* __restrict__ deg_ptr, const int32_t* __restrict__ deg_src,
-                         float* __restrict__ kin) {
+                         const int32_t* __restrict__ deg_eid, float* __restrict__ kin) {
   const int64_t per_row = (int64_t)n_rel * n0;
   int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (idx >= rows * per_row) return;
@@ -537,9 +539,13 @@ __global__ void k_degree(const uint32_t* __restrict__ bits, int64_t rows, int wo
   const int rem = static_cast<int>(idx - b * per_row);
   const int r = rem / n0, p = rem - r * n0;
   const uint32_t* row = bits + b * words;
+  const int* pp = deg_ptr + (int64_t)r * (n0 + 1);
   float out = -1.f;
-  if (bit_of(row, f0_node[p])) {
-    const int* pp = deg_ptr + (int64_t)r * (n0 + 1);
+  if (deg_eid) {
+    int c = 0;
+    for (int e = pp[p]; e < pp[p + 1]; ++e) c += bit_of(row, deg_eid[e]);
+    out = static_cast<float>(c);
+  } else if (bit_of(row, f0_node[p])) {
     int c = 0;
     for (int e = pp[p]; e < pp[p + 1]; ++e) c += bit_of(row, deg_src[e]);
     out = static_cast<float>(c);
@@ -570,6 +576,13 @@ struct AggArgs {
   int f_real;
   const int32_t* tgt_type;      // multi-node-type plans: node type of each target (else null)
   int dst_type[XPG_MAX_TERMS];  // term k reaches only targets of this type (-1: every target)
+  // edge masks (agg_eid != null): in-edge e kept iff bit agg_eid[e] of the row; MEAN self term =
+  // number of kept self-loop edges (self_ptr / self_eid)
+  const uint32_t* bits;
+  int words;
+  const int32_t* agg_eid;
+  const int32_t* self_ptr;
+  const int32_t* self_eid;
 };
 
 __device__ __forceinline__ float inv_sqrt_deg(float kin) {
@@ -621,6 +634,7 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
     } else {
       const float kt = kb[(int64_t)r * a.n0 + t0];
       const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+      const uint32_t* brow = a.agg_eid ? a.bits + b * a.words : nullptr;
       if (kind == XPG_TERM_GCN) {
         const float dt = inv_sqrt_deg(kt);
         const float cself = dt * dt;
@@ -630,7 +644,7 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
           for (int e = pp[t]; e < pp[t + 1]; ++e) {
             const int u0 = a.agg_f0[e];
             const float ku = kb[(int64_t)r * a.n0 + u0];
-            if (ku >= 0.f) {
+            if (brow ? bit_of(brow, a.agg_eid[e]) : ku >= 0.f) {
               const float c = inv_sqrt_deg(ku) * dt;
               const int up = L1 ? u0 : a.agg_src[e];
               const float4* src = reinterpret_cast<const float4*>(base + (int64_t)up * a.width);
@@ -641,13 +655,19 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
         }
       } else {  // MEAN
         if (kt >= 0.f) {
-          const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+          int sm = 0;
+          if (brow) {
+            const int* sp = a.self_ptr + (int64_t)r * (a.n_tgt + 1);
+            for (int e = sp[t]; e < sp[t + 1]; ++e) sm += bit_of(brow, a.self_eid[e]);
+          } else {
+            sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+          }
           const float cnt = kt + static_cast<float>(sm);
 #pragma unroll
           for (int j = 0; j < NV; ++j) fma4(s[j], static_cast<float>(sm), selfrow[sub + j * LPS]);
           for (int e = pp[t]; e < pp[t + 1]; ++e) {
             const int u0 = a.agg_f0[e];
-            if (kb[(int64_t)r * a.n0 + u0] >= 0.f) {
+            if (brow ? bit_of(brow, a.agg_eid[e]) : kb[(int64_t)r * a.n0 + u0] >= 0.f) {
               const int up = L1 ? u0 : a.agg_src[e];
               const float4* src = reinterpret_cast<const float4*>(base + (int64_t)up * a.width);
 #pragma unroll
@@ -692,6 +712,19 @@ __global__ void k_take_col(const float* __restrict__ C, int64_t M, int64_t ldc, 
                            float* __restrict__ y) {
   int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (m < M) y[m] = C[m * ldc + col];
+}
+
+// Link decoder of edge problems: y[r] = act(sum_f C[r][a][f] C[r][b][f]) over the n real columns
+// of the last layer (the query edge's endpoint rows a, b of mask row r), fixed fma order.
+__global__ void k_edge_dot(const float* __restrict__ C, int64_t rows, int n_tgt, int64_t ldc, int n, int ta,
+                           int tb, int act, float* __restrict__ y) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const float* ca = C + (r * n_tgt + ta) * ldc;
+  const float* cb = C + (r * n_tgt + tb) * ldc;
+  float s = 0.f;
+  for (int f = 0; f < n; ++f) s = fmaf(ca[f], cb[f], s);
+  y[r] = act_apply(s, act);
 }
 
 // ------------------------------------------------------------------------------ fused forward
@@ -3283,6 +3316,7 @@ int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t r
   const char* env = getenv("XPG_FORWARD");
   if (!env || std::strcmp(env, "fused") != 0) return 1;
   if (p->n_layers > kFusedMaxLayers || p->n_head > kFusedMaxHead || plan_multi_type(p)) return 1;
+  if (p->edge_masks || p->edge_dot) return 1;  // edge problems: multi-kernel path only
   FusedArgs a;
   std::memset(&a, 0, sizeof(a));
   a.rows = rows;
@@ -3470,6 +3504,7 @@ int wide_layout(const xpg_forward_plan* p, WideWs* W) {
 }
 
 bool wide_wanted(const xpg_forward_plan* p) {
+  if (p->edge_masks || p->edge_dot) return false;  // edge problems: multi-kernel path only
   const char* env = getenv("XPG_FORWARD");
   if (env && std::strcmp(env, "wide") == 0) return true;
   if (env && *env) return false;  // another path forced
@@ -3616,6 +3651,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
 // Lanes-=-rows fused forward for 1- and 2-layer plans (returns 1 when it does not apply).
 int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
   if (p->n_layers < 1 || p->n_layers > 2 || p->n_head > kFusedMaxHead || plan_multi_type(p)) return 1;
+  if (p->edge_masks || p->edge_dot) return 1;  // edge problems: multi-kernel path only
   RowsFwdArgs a;
   std::memset(&a, 0, sizeof(a));
   a.rows = rows;
@@ -3939,8 +3975,9 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   const int words = words_of(p->cols);
   {
     const int64_t n = rows * (int64_t)p->n_rel * p->n0;
+    XPG_REQ(!p->edge_masks || p->deg_eid || p->n_deg_edges == 0, "masked_forward: edge-mask plan without deg_eid");
     hipLaunchKernelGGL(k_degree, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, st, bits, rows, words, p->n0,
-                       p->n_rel, p->f0_node, p->deg_ptr, p->deg_src, kin);
+                       p->n_rel, p->f0_node, p->deg_ptr, p->deg_src, p->edge_masks ? p->deg_eid : nullptr, kin);
     XPG_LAUNCHED();
   }
   for (int l = 0; l < p->n_layers; ++l) {
@@ -3962,6 +3999,14 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
     a.self_mult = ly.self_mult;
     a.n_terms = ly.n_terms;
     a.tgt_type = ly.tgt_type;
+    if (p->edge_masks) {
+      XPG_REQ(ly.agg_eid && ly.self_ptr && ly.self_eid, "masked_forward: edge-mask layer without edge columns");
+      a.bits = bits;
+      a.words = words;
+      a.agg_eid = ly.agg_eid;
+      a.self_ptr = ly.self_ptr;
+      a.self_eid = ly.self_eid;
+    }
     for (int k = 0; k < ly.n_terms; ++k) {
       a.kind[k] = ly.terms[k].kind;
       a.rel[k] = ly.terms[k].rel;
@@ -4009,8 +4054,16 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
     cur = nxt;
     cur_ld = hd.n_pad;
   }
-  hipLaunchKernelGGL(k_take_col, dim3(static_cast<unsigned>(cdiv(M, 256))), dim3(256), 0, st, cur, M, cur_ld,
-                     p->out_col, y);
+  if (p->edge_dot) {
+    const int n_real = p->n_head > 0 ? p->head[p->n_head - 1].n_real : last.f_out;
+    XPG_REQ(p->dot_a >= 0 && p->dot_a < last.n_tgt && p->dot_b >= 0 && p->dot_b < last.n_tgt,
+            "masked_forward: link decoder targets out of range");
+    hipLaunchKernelGGL(k_edge_dot, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, st, cur, rows,
+                       last.n_tgt, cur_ld, n_real, p->dot_a, p->dot_b, p->dot_act, y);
+  } else {
+    hipLaunchKernelGGL(k_take_col, dim3(static_cast<unsigned>(cdiv(M, 256))), dim3(256), 0, st, cur, M, cur_ld,
+                       p->out_col, y);
+  }
   XPG_LAUNCHED();
   return XPG_OK;
 }

@@ -149,6 +149,32 @@ class Data:
             sub_names = names_arr[torch.where(emask)[0].cpu().numpy()].tolist()
         return sub_feat, sub_ei, sub_names, sub_ind, sub_nt, sub_et
 
+    def edge_comp_graph(self, ind, n_hops, names):
+        """Computational graph of an edge problem (edge masks mode; the reference's data.py:281-361
+        hands the edge index to k_hop_subgraph as a node id, so its edge path is broken): nodes
+        within n_hops + 1 hops of either endpoint of edge `ind`, every edge with both ends inside
+        (original order), relabelled.  Returns (sub_feat, sub_edge_index, sub_names = the kept
+        edges' names, sub_ind = position of edge `ind` among them, (u, v) relabelled)."""
+        hops = n_hops + 1
+        ei = self.edge_index
+        n = self.feat.shape[0]
+        if not 0 <= int(ind) < ei.shape[1]:
+            raise IndexError(f"edge {ind} out of range for {ei.shape[1]} edges")
+        u, v = int(ei[0, ind]), int(ei[1, ind])
+        node = torch.zeros(n, dtype=torch.bool, device=ei.device)
+        for seed in (u, v):
+            subset, _, _, _ = k_hop_subgraph(seed, hops, ei, n)
+            node[subset] = True
+        subset = torch.nonzero(node).reshape(-1)
+        remap = torch.full((n,), -1, dtype=torch.long, device=ei.device)
+        remap[subset] = torch.arange(subset.numel(), device=ei.device)
+        keep = node[ei[0]] & node[ei[1]]
+        pos = torch.nonzero(keep).reshape(-1)
+        sub_ind = int(torch.nonzero(pos == int(ind)).reshape(-1)[0])
+        sub_names = np.array(names, dtype=str)[pos.cpu().numpy()].tolist()
+        return (self.feat[subset], remap[ei[:, keep]], sub_names, sub_ind,
+                (int(remap[u]), int(remap[v])))
+
     def element_size(self, problem):
         """data.py:363-388."""
         return self.edge_index.shape[1] if "edge" in problem else self.feat.shape[0]

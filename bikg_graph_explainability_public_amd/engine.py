@@ -193,14 +193,18 @@ def dense(A: torch.Tensor, W: torch.Tensor, bias, act=None, n_real=None) -> torc
 
 
 # ----------------------------------------------------------------------------- forward plan
-def plan_arrays(S, rel_np, queries, L):
+def plan_arrays(S, rel_np, queries, L, rel_eid=None):
     """Receptive-field frontiers and CSR arrays (numpy; see include/xpgnn.h).
 
     frontiers[L] = queries; frontiers[l-1] = frontiers[l] + sorted new in-neighbours (all
     relations), so frontiers[l] is a prefix of frontiers[l-1].  deg_*: in-edges (self-loops
     excluded) of every F_0 node per relation, relation-major with absolute offsets.  layers[l-1]:
     in-edges of F_l targets (self-loops excluded) with source positions in F_{l-1} and F_0, plus
-    the multiplicity of (t, t) edges per relation."""
+    the multiplicity of (t, t) edges per relation.
+
+    rel_eid (edge-mask plans, Data.perturb_edge): per relation the mask column of every edge;
+    the CSRs then also carry each entry's column (deg_eid, agg_eid) and every target's
+    self-loop columns (self_ptr / self_eid)."""
     all_src = np.concatenate([e[0] for e in rel_np]) if rel_np else np.zeros(0, np.int64)
     all_dst = np.concatenate([e[1] for e in rel_np]) if rel_np else np.zeros(0, np.int64)
     fr = [None] * (L + 1)
@@ -222,58 +226,91 @@ def plan_arrays(S, rel_np, queries, L):
         pos.append(p)
     n0 = fr[0].size
 
+    eids = rel_eid if rel_eid is not None else [np.zeros(e.shape[1], np.int64) for e in rel_np]
+
     def csr(targets_pos, n_t, src_pos_maps):
         ptrs, cols, off = [], [[] for _ in src_pos_maps], 0
-        smul = []
-        for s, d in rel_np:
+        smul, eid, sptr, seid, soff = [], [], [], [], 0
+        for (s, d), ecol in zip(rel_np, eids):
             k = s != d
-            s2, d2 = s[k], d[k]
+            s2, d2, e2 = s[k], d[k], ecol[k]
             sel = targets_pos[d2] >= 0
             key = targets_pos[d2[sel]]
             order = np.argsort(key, kind="stable")
             src_nodes = s2[sel][order]
+            eid.append(e2[sel][order])
             for j, m in enumerate(src_pos_maps):
                 cols[j].append(m(src_nodes))
             cnt = np.bincount(key, minlength=n_t)
             ptrs.append(np.concatenate([[0], np.cumsum(cnt)]) + off)
             off += int(cnt.sum())
-            loops = s[~k]
+            loops, lcol = s[~k], ecol[~k]
             ls = targets_pos[loops] >= 0
-            smul.append(np.bincount(targets_pos[loops[ls]], minlength=n_t))
+            lkey = targets_pos[loops[ls]]
+            smul.append(np.bincount(lkey, minlength=n_t))
+            lorder = np.argsort(lkey, kind="stable")
+            seid.append(lcol[ls][lorder])
+            sptr.append(np.concatenate([[0], np.cumsum(smul[-1])]) + soff)
+            soff += int(smul[-1].sum())
         cat = [np.concatenate(c) if c else np.zeros(0, np.int64) for c in cols]
-        return np.concatenate(ptrs), cat, np.concatenate(smul)
+        return (np.concatenate(ptrs), cat, np.concatenate(smul), np.concatenate(eid),
+                np.concatenate(sptr), np.concatenate(seid))
 
-    deg_ptr, (deg_src,), _ = csr(pos[0], n0, [lambda v: v])
+    deg_ptr, (deg_src,), _, deg_eid, _, _ = csr(pos[0], n0, [lambda v: v])
     layers = []
     for lvl in range(1, L + 1):
-        ptr_, (a_src, a_f0), smul = csr(pos[lvl], fr[lvl].size,
-                                        [lambda v, l=lvl: pos[l - 1][v], lambda v: pos[0][v]])
-        layers.append({"agg_ptr": ptr_, "agg_src": a_src, "agg_f0": a_f0, "self_mult": smul})
+        ptr_, (a_src, a_f0), smul, a_eid, s_ptr, s_eid = csr(
+            pos[lvl], fr[lvl].size, [lambda v, l=lvl: pos[l - 1][v], lambda v: pos[0][v]])
+        layers.append({"agg_ptr": ptr_, "agg_src": a_src, "agg_f0": a_f0, "self_mult": smul,
+                       "agg_eid": a_eid, "self_ptr": s_ptr, "self_eid": s_eid})
     return {"frontiers": fr, "pos": pos, "deg_ptr": deg_ptr, "deg_src": deg_src,
-            "layers": layers}
+            "deg_eid": deg_eid, "layers": layers}
 
 
 class ForwardPlan:
     """Receptive-field plan of one (subgraph, model program, query set)."""
 
-    def __init__(self, program, sub_feat, rel_edges, queries, device=None, node_type=None):
+    def __init__(self, program, sub_feat, rel_edges, queries, device=None, node_type=None,
+                 edge_cols=None, link=None):
         """`node_type` ([S] node type of every subgraph node) is required by multi-node-type
-        programs: per layer, every target's type gates the relation terms (xpgnn.h)."""
+        programs: per layer, every target's type gates the relation terms (xpgnn.h).
+
+        Edge problems (Data.perturb_edge, data.py:500-554): `edge_cols` = per relation the mask
+        column of every edge (mask columns are the subgraph's edges; `cols` becomes their
+        count) and `link` = (a, b, act): the output is the link decoder act(<h_a, h_b>) of
+        queries a and b instead of one column per query."""
         device = torch.device(device) if device is not None else sub_feat.device
         _lib.require_device(torch.empty(0, device=device), "plan device")
         if len(program.convs) == 0:
             raise ValueError("program has no conv layer")
         self.device = device
         self.program = program
-        self.cols = int(sub_feat.shape[0])
-        S = self.cols
+        S = int(sub_feat.shape[0])  # subgraph nodes
         self.n_rel = len(rel_edges)
         self._keep = []  # device tensors referenced by descriptors
 
         rel_np = [np.asarray(e.detach().cpu().numpy(), dtype=np.int64).reshape(2, -1)
                   for e in rel_edges]
+        rel_eid = None
+        if edge_cols is not None:
+            rel_eid = [np.asarray(torch.as_tensor(c).detach().cpu().numpy(), dtype=np.int64).reshape(-1)
+                       for c in edge_cols]
+            if len(rel_eid) != len(rel_np) or any(c.size != e.shape[1] for c, e in zip(rel_eid, rel_np)):
+                raise ValueError("edge_cols must give one mask column per edge of every relation")
+            if program.n_types > 1:
+                raise ValueError("edge masks on multi-node-type programs are not supported")
+        self.edge_masks = rel_eid is not None
+        self.cols = (int(max((int(c.max()) for c in rel_eid if c.size), default=-1)) + 1
+                     if self.edge_masks else S)
+        if self.edge_masks:
+            ncol = sum(c.size for c in rel_eid)
+            allc = np.concatenate(rel_eid) if ncol else np.zeros(0, np.int64)
+            if ncol and (allc.min() < 0 or np.unique(allc).size != ncol or self.cols != ncol):
+                raise ValueError("edge mask columns must be 0..E-1, one per edge")
+            if ncol == 0:
+                raise ValueError("edge masks need at least one edge")
         L = len(program.convs)
-        arr = plan_arrays(S, rel_np, queries, L)
+        arr = plan_arrays(S, rel_np, queries, L, rel_eid)
         self.arrays = arr
         fr = arr["frontiers"]
         n0 = fr[0].size
@@ -320,6 +357,11 @@ class ForwardPlan:
             ld.agg_src = self._i32(lay["agg_src"] if lay["agg_src"].size else np.zeros(1)).data_ptr()
             ld.agg_f0 = self._i32(lay["agg_f0"] if lay["agg_f0"].size else np.zeros(1)).data_ptr()
             ld.self_mult = self._i32(lay["self_mult"]).data_ptr()
+            if self.edge_masks:
+                nz = lambda a: a if a.size else np.zeros(1)
+                ld.agg_eid = self._i32(nz(lay["agg_eid"])).data_ptr()
+                ld.self_ptr = self._i32(lay["self_ptr"]).data_ptr()
+                ld.self_eid = self._i32(nz(lay["self_eid"])).data_ptr()
             n_types = program.n_types
             bias = torch.zeros((n_types, f_out_pad), dtype=torch.float32, device=device)
             bias[:, :conv.f_out] = conv.bias.to(device).reshape(-1, conv.f_out)
@@ -367,11 +409,23 @@ class ForwardPlan:
 
         self.n_out = fr[L].size
         self.desc = ForwardPlanDesc(
-            cols=S, n_rel=self.n_rel, n0=n0, f0_node=self._f0_node.data_ptr(),
+            cols=self.cols, n_rel=self.n_rel, n0=n0, f0_node=self._f0_node.data_ptr(),
             deg_ptr=self._deg_ptr.data_ptr(), deg_src=self._deg_src.data_ptr(),
             n_deg_edges=int(arr["deg_src"].size), n_layers=L,
             layers=self._layers, n_head=len(program.head), head=self._head,
             out_col=program.out_col)
+        if self.edge_masks:
+            self.desc.edge_masks = 1
+            self.desc.deg_eid = self._i32(arr["deg_eid"] if arr["deg_eid"].size
+                                          else np.zeros(1)).data_ptr()
+        self.link = link
+        if link is not None:
+            a, b, act = link
+            if not (0 <= a < self.n_out and 0 <= b < self.n_out):
+                raise ValueError("link decoder targets out of range")
+            self.desc.edge_dot, self.desc.dot_a, self.desc.dot_b = 1, int(a), int(b)
+            self.desc.dot_act = ACT[act]
+            self.n_out = 1
         self._ws = None
 
     def _i32(self, a):

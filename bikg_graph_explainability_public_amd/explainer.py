@@ -56,6 +56,14 @@ class Explainer:
         self.last_run = None  # diagnostics of the last run (per-repeat losses, path used)
         self.group = None     # torch.distributed process group for multi-GPU runs (None = world)
 
+    @property
+    def edge_masks(self):
+        """Non-compat edge problems (params["edge_masks"] = True): mask columns
+        are the computational graph's edges (Data.perturb_edge, data.py:500-554) and the arch is
+        an edge-level model (nn.LinkModel).  Off (default), edge problems fail as the reference's
+        do (masks.py:294)."""
+        return "edge" in self.problem and bool(self.params.get("edge_masks", False))
+
     @staticmethod
     def initial_assertions(feat, edge_index, arch, params, names, pathways, pathway_names,
                            element_type, problem):
@@ -137,7 +145,19 @@ class Explainer:
         data = Data(feat, ei)
         sub_pw = sub_pw_names = None
         sub_nt = sub_et = None
-        if "graph" not in self.problem:
+        link = None
+        if self.edge_masks:
+            # edge problem, edge masks (non-compat: the reference's edge path is broken at
+            # masks.py:294 and data.py:331): mask columns = the computational graph's edges
+            if h_etypes is not None or node_types is not None or edge_types is not None:
+                raise NotImplementedError("edge masks: homogeneous graphs only")
+            n_hops = Model(self.arch).get_hops(0)
+            ind = self.extract_index(element, names)
+            sub_feat, sub_ei, sub_names, sub_ind, link = data.edge_comp_graph(ind, n_hops, names)
+            if pathways is not None:
+                sub_pw, sub_pw_names, _ = Pathways(pathways, pathway_names,
+                                                   pathway_types).comp_graph(sub_names)
+        elif "graph" not in self.problem:
             rels = len(h_etypes) if h_etypes is not None else 0
             n_hops = Model(self.arch).get_hops(rels)
             ind = self.extract_index(element, names)
@@ -153,7 +173,7 @@ class Explainer:
             sub_et = edge_types.clone() if edge_types is not None else None
             if pathways is not None:
                 sub_pw, sub_pw_names = pathways, pathway_names
-        if "graph" not in self.problem and (self.element_type is not None or
+        if "graph" not in self.problem and not self.edge_masks and (self.element_type is not None or
                                             self.node_types is not None or
                                             self.edge_types is not None):
             filt = self.filter_hetero_names(sub_names, sub_nt, sub_et, h_ntypes, h_etypes)
@@ -168,7 +188,7 @@ class Explainer:
         if isinstance(sub_ind, torch.Tensor):
             sub_ind = int(sub_ind.reshape(-1)[0])
         S = Data(sub_feat, sub_ei).element_size(self.problem)
-        return {"sub_feat": sub_feat, "sub_ei": sub_ei, "sub_names": sub_names,
+        return {"link": link, "sub_feat": sub_feat, "sub_ei": sub_ei, "sub_names": sub_names,
                 "sub_ind": sub_ind, "sub_nt": sub_nt, "sub_et": sub_et, "h_ntypes": h_ntypes,
                 "h_etypes": h_etypes, "padded_dims": padded_dims, "sub_pw": sub_pw,
                 "sub_pw_names": sub_pw_names, "sub_pw_inds": sub_pw_inds, "S": S,
@@ -191,9 +211,14 @@ class Explainer:
         sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
 
-        plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, [sub_ind], *geo)
+        if self.edge_masks:
+            plan = pipeline.build_edge_plan(self.arch, sub_feat, sub_ei, *c["link"])
+            verify = lambda: pipeline.verify_edge_plan(plan, self.arch, sub_feat, sub_ei, *c["link"])
+        else:
+            plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, [sub_ind], *geo)
+            verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo)
         if plan is not None and self.params.get("verify_arch", True):
-            ok, err = pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo)
+            ok, err = verify()
             if not ok:
                 warnings.warn(f"compiled arch disagrees with its torch forward (max err {err:.3g});"
                               " using the generic torch path")
@@ -205,11 +230,15 @@ class Explainer:
         # RNG order (mask_generator -> LinearRegression init -> DataLoader seed, per repeat);
         # then run all repeats' forward / KernelSHAP / surrogate fits as batched launches.
         bits_list, w0_list, masks = [], [], []
-        on_device = sampler == "device" and "edge" not in self.problem
+        on_device = sampler == "device" and ("edge" not in self.problem or self.edge_masks)
+        # edge masks: the samplers see S = edge count columns (the element size of
+        # data.py:383-385) through a node-problem Mask over an [S, 1] placeholder feature
+        mfeat = torch.zeros((S, 1), device=device) if self.edge_masks else sub_feat
+        mproblem = "node_prediction" if self.edge_masks else self.problem
         if on_device and c["sub_pw_inds"] is not None:
             # device community sampler: the block plan and column -> community CSR are
             # repeat-invariant; each repeat draws a new seed (masks.py:262-397)
-            cmask = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params, self.problem)
+            cmask = Mask(mfeat, sub_ei, c["sub_pw_inds"], self.params, mproblem)
             cplan = cmask.community_plan()
             ctabs = engine.community_tables(cplan, c["sub_pw_inds"], S, device)
         for _ in range(times):
@@ -224,8 +253,8 @@ class Explainer:
                                                            device, tables=ctabs)[0])
                 masks.append(None)
             else:
-                mask, _ = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,
-                               self.problem).generate()
+                mask, _ = Mask(mfeat, sub_ei, c["sub_pw_inds"], self.params,
+                               mproblem).generate()
                 mask = mask.to(device)
                 bits_list.append(engine.pack_masks(mask))
                 masks.append(mask)
@@ -252,6 +281,14 @@ class Explainer:
                 empty = pipeline.empty_copy_rows(flat, S, sub_ei).reshape(times, R)
                 y = torch.stack([pipeline.multi_type_targets(y[i], empty[i], batch, sub_ind, S, q4)
                                  for i in range(times)])
+        elif self.edge_masks:
+            def generic(t0, t1):
+                ys = [pipeline.generic_edge_outputs(
+                    self.arch, sub_feat, sub_ei,
+                    engine.unpack_masks(bits_list[i], S) if masks[i] is None else masks[i],
+                    *c["link"], max_rows=batch) for i in range(t0, t1)]
+                return torch.stack(ys) if ys else torch.empty((0, R), device=device)
+            y = sharding.gather_map(times, generic, g)
         else:
             def generic(t0, t1):
                 ys = [pipeline.generic_outputs(

@@ -295,3 +295,27 @@ class HeteroSageStack(nn.Module):
         for layer in self.fc:
             x = layer(x)
         return x
+
+
+class LinkModel(nn.Module):
+    """Edge-level model for edge problems: a node encoder (e.g. ConvStack with
+    final_act="identity") and a dot-product link decoder, score(u, v) = act(<z_u, z_v>).
+
+    forward(x, edge_index, edge_label_index=None) runs the encoder's message passing over
+    `edge_index` and scores the edges of `edge_label_index` (default: every edge of
+    `edge_index`) — the per-edge output the reference's edge problem extracts
+    (model.py:295-328).  Scoring a separate label index keeps the query edge's output defined
+    when Data.perturb_edge (data.py:500-554) removes that edge from the message passing."""
+
+    def __init__(self, encoder, act="sigmoid"):
+        super().__init__()
+        if act not in ("sigmoid", "identity", None):
+            raise ValueError("LinkModel act must be 'sigmoid' or 'identity'")
+        self.encoder = encoder
+        self.act = act or "identity"
+
+    def forward(self, x, edge_index, edge_label_index=None):
+        z = self.encoder(x, edge_index)
+        eli = edge_index if edge_label_index is None else edge_label_index
+        s = (z[eli[0]] * z[eli[1]]).sum(-1, keepdim=True)
+        return torch.sigmoid(s) if self.act == "sigmoid" else s

@@ -45,6 +45,9 @@ def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
     except UnsupportedArch as e:
         warnings.warn(f"engine cannot compile arch ({e}); using the generic torch path")
         return None
+    if prog.link_act is not None:
+        raise ValueError("a LinkModel scores edges: explain it with problem='edge_prediction' "
+                         "and params['edge_masks'] = True")
     x = feat
     nt = None
     if multi:
@@ -65,6 +68,61 @@ def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
         return None
     plan.multi_type = multi
     return plan
+
+
+def build_edge_plan(arch, feat, edge_index, u, v):
+    """ForwardPlan of an edge problem (edge masks, Data.perturb_edge data.py:500-554): mask
+    columns = the subgraph's edges, output = the LinkModel decoder's score of edge (u, v).
+    None when the engine cannot compile `arch` (generic torch path)."""
+    try:
+        prog = compile_arch(arch)
+    except UnsupportedArch as e:
+        warnings.warn(f"engine cannot compile arch ({e}); using the generic torch path")
+        return None
+    if prog.link_act is None:
+        warnings.warn("edge masks need an edge-level model (nn.LinkModel); using the generic "
+                      "torch path")
+        return None
+    queries, link = ([u, v], (0, 1, prog.link_act)) if u != v else ([u], (0, 0, prog.link_act))
+    cols = torch.arange(edge_index.shape[1], device=edge_index.device)
+    try:
+        return engine.ForwardPlan(prog, feat, [edge_index], queries, edge_cols=[cols], link=link)
+    except ValueError as e:
+        warnings.warn(f"engine plan rejected ({e}); using the generic torch path")
+        return None
+
+
+def generic_edge_outputs(arch, feat, edge_index, mask, u, v, max_rows=None):
+    """Edge problem through the user's module (torch, on the device): the B-fold union graph of
+    Data.perturbator with perturb_edge (data.py:591-648, 500-554: copy b keeps edge e iff
+    mask[b, e], copy-major order, node ids shifted by b * N) and `arch(x, ei,
+    edge_label_index=...)` scoring each copy's (u, v) -> y [B]."""
+    B, _ = mask.shape
+    N = feat.shape[0]
+    step = B if max_rows is None else max_rows
+    ys = []
+    for b0 in range(0, B, step):
+        m = mask[b0:b0 + step]
+        nb = m.shape[0]
+        rows, cols = torch.nonzero(m, as_tuple=True)
+        ei = edge_index[:, cols] + rows * N
+        x = feat.repeat(nb, 1).float()
+        off = torch.arange(nb, device=feat.device) * N
+        eli = torch.stack([off + u, off + v])
+        with torch.no_grad():
+            ys.append(arch(x, ei, edge_label_index=eli).reshape(-1).float())
+    return torch.cat(ys)
+
+
+def verify_edge_plan(plan, arch, feat, edge_index, u, v, rows=8, tol=1e-4):
+    """The compiled edge plan against the user's module on a few random edge masks."""
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    mask = (torch.rand((rows, edge_index.shape[1]), generator=g) < 0.5).to(feat.device)
+    mask[0] = True
+    ref = generic_edge_outputs(arch, feat, edge_index, mask, u, v)
+    got = plan.forward(engine.pack_masks(mask))[:, 0]
+    err = (ref - got).abs().max().item()
+    return err <= tol * max(1.0, ref.abs().max().item()), err
 
 
 def empty_copy_rows(bits, cols, edge_index, max_bytes=256 << 20):

@@ -62,6 +62,7 @@ class ModelProgram:
     out_col: int = 0
     n_types: int = 1               # > 1: multi-node-type program (node-type-gated terms)
     out_type: Optional[int] = None  # multi-node-type: node type whose rows feed the head
+    link_act: Optional[str] = None  # LinkModel: the program is its encoder; decoder act(<z_u, z_v>)
 
     @property
     def hops(self):
@@ -227,6 +228,10 @@ def compile_arch(arch: nn.Module, edge_type_names=None, node_type_names=None) ->
     """Lower `arch` to a ModelProgram.  `edge_type_names` (list of (src, rel, dst) tuples in
     homogenised edge-type order, data.py:743-822) enables HeteroConv relations;
     `node_type_names` with two or more types selects the multi-node-type lowering."""
+    if type(arch).__name__ == "LinkModel" and hasattr(arch, "encoder"):
+        prog = compile_arch(arch.encoder, edge_type_names, node_type_names)
+        prog.link_act = getattr(arch, "act", "identity") or "identity"
+        return prog
     rel_index = None
     if edge_type_names is not None:
         rel_index = {tuple(et): i for i, et in enumerate(edge_type_names)}

@@ -22,7 +22,9 @@
  *   xpg_masked_forward                 — Data.perturbator + Model.infer + extract_node_edge_output
  *                                        (wlm.py:349-436 -> data.py:591-648, model.py:62-116,
  *                                        model.py:295-328) for GCNConv / SAGEConv / HeteroConv-sum
- *                                        conv stacks with a dense head
+ *                                        conv stacks with a dense head; with edge_masks set, the
+ *                                        edge problem's Data.perturb_edge (data.py:500-554: mask
+ *                                        columns are edges) and a dot-product link decoder
  *   xpg_dense                          — the dense feature x weight contraction inside each layer
  *                                        (PyG Linear / GCNConv.lin / SAGEConv.lin_l|lin_r)
  *   xpg_wlm_fit                        — train_model's epoch loop     wlm.py:132-278 with
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 9
+#define XPG_ABI_VERSION 10
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -136,6 +138,10 @@ typedef struct xpg_layer_desc {
   const int32_t* tgt_type; /* multi-node-type plans: [n_tgt] node type of each target;   */
                            /* NULL for homogeneous / single-node-type graphs             */
   int32_t n_types;         /* rows of bias (1 when tgt_type is NULL)                   */
+  /* edge-mask plans only (plan.edge_masks = 1; NULL otherwise):                          */
+  const int32_t* agg_eid;  /* [n_edges] mask column (subgraph edge id) of each in-edge   */
+  const int32_t* self_ptr; /* [n_rel * (n_tgt + 1)] self-loop edges of each target       */
+  const int32_t* self_eid; /* their mask columns (MEAN terms count the kept ones)        */
 } xpg_layer_desc;
 
 typedef struct xpg_head_desc {
@@ -157,12 +163,26 @@ typedef struct xpg_forward_plan {
   int32_t n_head;
   const xpg_head_desc* head;      /* host array [n_head]                               */
   int32_t out_col;         /* output column extracted (0)                              */
+  /* Edge masks (Data.perturb_edge, data.py:500-554): mask columns are the subgraph's edges
+   * (cols = edge count) and edge e is kept in row r iff its bit is set; every node stays
+   * active.  Degrees and aggregations test the edge's own bit (deg_eid / agg_eid / self_eid);
+   * GCN keeps one weight-1 self-loop per node whatever the mask (add_remaining_self_loops),
+   * MEAN counts the kept self-loop edges.  Only the multi-kernel path takes these plans. */
+  int32_t edge_masks;      /* 0: node masks (default), 1: edge masks                   */
+  const int32_t* deg_eid;  /* [n_deg_edges] mask column of each deg_src entry          */
+  /* Link decoder (edge problems): y[r] = act(<h_a, h_b>) over the n_real columns of the
+   * last layer (head output, else last conv) of last-frontier targets a and b, instead of
+   * one output column per target (then y has 1 column). */
+  int32_t edge_dot;        /* 0: per-target outputs (default), 1: dot-product decoder   */
+  int32_t dot_a, dot_b;    /* target positions in the last frontier                   */
+  int32_t dot_act;         /* enum xpg_act applied to the dot product                  */
 } xpg_forward_plan;
 
 /* Workspace needed by xpg_masked_forward for `rows` mask rows. */
 int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* bytes);
 /* y[r * n_last + i] = model output (column out_col) of target i of the last conv layer for
- * mask row r (n_last = layers[n_layers-1].n_tgt; 1 for a single query). */
+ * mask row r (n_last = layers[n_layers-1].n_tgt; 1 for a single query); with edge_dot set,
+ * y[r] = the decoded score of the target pair (dot_a, dot_b). */
 int xpg_masked_forward(const xpg_forward_plan* plan, const uint32_t* bits, int64_t rows,
                        float* y, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
 

@@ -1,0 +1,223 @@
+"""Edge problems with edge masks (non-compat flag params["edge_masks"]).
+
+The reference's edge path is unreachable end to end (masks.py:294 reads a missing attribute,
+data.py:331 hands the edge index to k_hop_subgraph as a node id).  Its intended semantics are
+restated by the oracle: mask columns = the computational graph's edges, copy b keeps edge e iff
+mask[b, e] (Data.perturb_edge, data.py:500-554), features never masked (data.py:582), and the
+explained output is an edge-level model's score of the query edge (nn.LinkModel: encoder +
+dot-product decoder).  Parity is pinned against the oracle and the torch module (parity of this
+path against the reference itself is unpinned: the reference cannot run it).
+
+CPU tests: oracle vs the torch LinkModel (the generic path), plan CSR edge columns, the edge
+computational graph.  GPU tests (-m gpu): the HIP multi-kernel path's edge-mask forward vs the
+oracle (atol 1e-5) and Explainer.run end to end vs the oracle pipeline (atol 1e-4)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from golden_utils import oracle_spec
+
+DEV = torch.device("cuda", 0)
+
+
+def _link(kind, dims, fc, seed=0):
+    from bikg_graph_explainability_public_amd.nn import ConvStack, LinkModel
+    torch.manual_seed(seed)
+    enc = ConvStack(kind, dims, fc, final_act="identity").eval()
+    return LinkModel(enc, act="sigmoid").eval()
+
+
+def _spec(kind, dims, fc, model):
+    sd = {k[len("encoder."):]: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    spec = oracle_spec({"arch_spec": {"kind": kind, "dims": dims, "fc": fc}}, sd)
+    if spec["fc"]:
+        spec["fc"][-1]["act"] = None  # encoder ends in Identity; the decoder applies the sigmoid
+    else:
+        spec["convs"][-1]["act"] = "relu"
+    return spec
+
+
+def _graph(S, E, seed, loops=True, dups=True):
+    rng = np.random.default_rng(seed)
+    ei = rng.integers(0, S, size=(2, E)).astype(np.int64)
+    if loops:
+        ei[:, :5] = ei[0, :5]            # self-loops
+    if dups:
+        ei[:, 5:10] = ei[:, 10:15]       # duplicate edges
+    return ei
+
+
+def _masks(R, E, seed):
+    rng = np.random.default_rng(seed)
+    m = rng.random((R, E)) < rng.uniform(0.2, 0.9, (R, 1))
+    m[0] = True
+    m[1] = False
+    return m
+
+
+ARCHS = [("gcn", [12, 16, 16], [16, 8]), ("sage", [12, 16, 16], [16, 8]),
+         ("gcn", [12, 16], [16]), ("sage", [12, 24], [24, 16, 8])]
+
+
+# ------------------------------------------------------------------------------------ CPU
+@pytest.mark.parametrize("kind,dims,fc", ARCHS)
+def test_oracle_edge_outputs_match_torch_linkmodel(kind, dims, fc):
+    """oracle.masked_edge_outputs (perturb_edge union graph + encoder + decoder) == the torch
+    LinkModel through pipeline.generic_edge_outputs on the same masks (CPU)."""
+    from bikg_graph_explainability_public_amd import pipeline
+    S, E = 40, 120
+    ei = _graph(S, E, 3)
+    x = np.random.default_rng(4).standard_normal((S, dims[0])).astype(np.float32)
+    model = _link(kind, dims, fc)
+    m = _masks(24, E, 5)
+    for u, v in [(int(ei[0, 20]), int(ei[1, 20])), (int(ei[0, 2]), int(ei[1, 2]))]:
+        ref = oracle.masked_edge_outputs(_spec(kind, dims, fc, model), x, ei, m, u, v)
+        got = pipeline.generic_edge_outputs(model, torch.from_numpy(x), torch.from_numpy(ei),
+                                            torch.from_numpy(m), u, v).numpy()
+        np.testing.assert_allclose(got, ref, atol=2e-6)
+
+
+def test_perturb_edge_known_answer():
+    """data.py:500-554 on a hand example: copy-major, node ids shifted by b * N, edge kept iff
+    its mask bit is set."""
+    ei = np.array([[0, 1, 2], [1, 2, 0]])
+    m = np.array([[1, 0, 1], [0, 1, 1]], dtype=bool)
+    pei, et = oracle.perturb_edge(m, ei, 3, edge_type=np.array([7, 8, 9]))
+    np.testing.assert_array_equal(pei, [[0, 2, 4, 5], [1, 0, 5, 3]])
+    np.testing.assert_array_equal(et, [7, 9, 8, 9])
+
+
+def test_plan_arrays_edge_columns():
+    """Edge-mask CSRs carry each entry's mask column; self-loops go to the self CSR."""
+    from bikg_graph_explainability_public_amd.engine import plan_arrays
+    ei = np.array([[0, 1, 2, 2, 3, 1], [1, 2, 1, 2, 1, 1]])
+    arr = plan_arrays(4, [ei], [1], 2, [np.arange(6)])
+    fr = arr["frontiers"]
+    assert fr[2].tolist() == [1] and fr[1].tolist() == [1, 0, 2, 3]
+    lay = arr["layers"][1]  # targets F_2 = {1}: in-edges 0->1 (col 0), 2->1 (col 2), 3->1 (col 4)
+    assert lay["agg_eid"].tolist() == [0, 2, 4]
+    assert lay["self_ptr"].tolist() == [0, 1] and lay["self_eid"].tolist() == [5]
+    # F_0 degrees: node order [1, 0, 2, 3]; node 2's in-edge 1->2 is column 1, loop 2->2 is out
+    deg = arr["deg_ptr"], arr["deg_eid"]
+    assert deg[1][deg[0][2]:deg[0][3]].tolist() == [1]
+
+
+def test_edge_comp_graph_matches_oracle():
+    from bikg_graph_explainability_public_amd.data import Data
+    S, E = 200, 500
+    ei = _graph(S, E, 9)
+    x = torch.randn(S, 4)
+    names = [f"e{i}" for i in range(E)]
+    for ind in (0, 17, 333):
+        sub_feat, sub_ei, sub_names, sub_ind, (u, v) = Data(x, torch.from_numpy(ei)).edge_comp_graph(
+            ind, 1, names)
+        subset, r_ei, pos, q, (ru, rv) = oracle.edge_comp_graph(ind, 1, ei, S)
+        np.testing.assert_array_equal(sub_ei.numpy(), r_ei)
+        assert sub_names == [names[p] for p in pos] and sub_ind == q and (u, v) == (ru, rv)
+        np.testing.assert_array_equal(sub_feat.numpy(), x.numpy()[subset])
+
+
+def test_edge_problem_without_flag_fails_like_reference():
+    """Default (compat) edge problems raise where the reference does (masks.py:294)."""
+    from bikg_graph_explainability_public_amd.masks import Mask
+    x = torch.randn(5, 3)
+    ei = torch.tensor([[0, 1], [1, 2]])
+    with pytest.raises(AttributeError):
+        Mask(x, ei, None, {"interpret_samples": 4, "epochs": 2}, "edge_prediction").generate()
+
+
+# ------------------------------------------------------------------------------------ GPU
+@pytest.fixture()
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from bikg_graph_explainability_public_amd import _lib
+    _lib.load()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,dims,fc", ARCHS)
+@pytest.mark.parametrize("query", [20, 2])  # a regular edge and a self-loop edge
+def test_engine_edge_forward_vs_oracle(_gpu, kind, dims, fc, query):
+    """HIP multi-kernel path with edge masks + link decoder vs the oracle (fp64), graphs with
+    self-loops and duplicate edges, all-on / all-off rows."""
+    from bikg_graph_explainability_public_amd import engine, pipeline
+    S, E = 60, 240
+    ei = _graph(S, E, 11)
+    x = np.random.default_rng(12).standard_normal((S, dims[0])).astype(np.float32)
+    model = _link(kind, dims, fc).to(DEV)
+    u, v = int(ei[0, query]), int(ei[1, query])
+    plan = pipeline.build_edge_plan(model, torch.from_numpy(x).to(DEV), torch.from_numpy(ei).to(DEV), u, v)
+    assert plan is not None and plan.edge_masks and plan.cols == E
+    m = _masks(300, E, 13)
+    y = plan.forward(engine.pack_masks(torch.from_numpy(m).to(DEV)))[:, 0].cpu().numpy()
+    ref = oracle.masked_edge_outputs(_spec(kind, dims, fc, model), x, ei, m, u, v)
+    np.testing.assert_allclose(y, ref, atol=1e-5)
+    ok, err = pipeline.verify_edge_plan(plan, model, torch.from_numpy(x).to(DEV),
+                                        torch.from_numpy(ei).to(DEV), u, v)
+    assert ok, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sampler", ["compat", "device"])
+def test_explainer_edge_masks_end_to_end_vs_oracle(_gpu, sampler):
+    """Explainer.run(edge name) with params["edge_masks"]: the computational graph's edges are
+    the mask columns; the repeats' weights equal the oracle pipeline (oracle forward on the
+    run's own masks, KernelSHAP, surrogate fit from the run's initial weights) to 1e-4, and the
+    DataFrame is indexed by the subgraph's edge names."""
+    from bikg_graph_explainability_public_amd import engine
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    S, E = 300, 1200
+    ei = _graph(S, E, 21)
+    x = np.random.default_rng(22).standard_normal((S, 12)).astype(np.float32)
+    kind, dims, fc = "sage", [12, 16, 16], [16, 8]
+    model = _link(kind, dims, fc)
+    names = [f"edge_{i}" for i in range(E)]
+    params = {"seed": 3, "interpret_samples": 16, "epochs": 10, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "edge_masks": True, "mask_sampler": sampler}
+    exp = Explainer(torch.from_numpy(x).to(DEV), torch.from_numpy(ei).to(DEV), model, params,
+                    names, problem="edge_prediction")
+    df, pdf = exp.run("edge_40", times=2)
+    assert pdf is None and exp.last_run["engine"]
+    _, r_ei, pos, q, (u, v) = oracle.edge_comp_graph(40, 2, ei, S)
+    assert exp.last_run["S"] == r_ei.shape[1] and set(df.index) == {names[p] for p in pos}
+    spec = _spec(kind, dims, fc, model)
+    sub_x = x[oracle.edge_comp_graph(40, 2, ei, S)[0]]
+    ws = []
+    for rep in exp.last_run["repeats"]:
+        m = engine.unpack_masks(rep["bits"], r_ei.shape[1]).cpu().numpy()
+        y_ref = oracle.masked_edge_outputs(spec, sub_x, r_ei, m, u, v)
+        np.testing.assert_allclose(rep["y"].cpu().numpy(), y_ref, atol=1e-5)
+        k_ref = oracle.shap_kernel(m)
+        w_ref, _, _ = oracle.train_wlm(m, rep["batch"], y_ref, k_ref, rep["w0"].cpu().numpy(),
+                                       params)
+        ws.append(w_ref)
+    mean = np.mean(ws, axis=0)
+    got = np.array([df.loc[names[p], "config_value_mean"] for p in pos])
+    np.testing.assert_allclose(got, mean, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_explainer_edge_masks_communities(_gpu):
+    """Edge communities (lists of edge names) through the device community sampler: community
+    scores are the means of their member edges' scores (pathways.py:387-429)."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    S, E = 200, 700
+    ei = _graph(S, E, 31)
+    x = np.random.default_rng(32).standard_normal((S, 12)).astype(np.float32)
+    model = _link("gcn", [12, 16, 16], [16, 8])
+    names = [f"edge_{i}" for i in range(E)]
+    _, r_ei, pos, q, _ = oracle.edge_comp_graph(7, 2, ei, S)
+    sub = [names[p] for p in pos]
+    comms = [sub[i::4] for i in range(4)]
+    params = {"seed": 5, "interpret_samples": 16, "epochs": 10, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "edge_masks": True, "mask_sampler": "device"}
+    exp = Explainer(torch.from_numpy(x).to(DEV), torch.from_numpy(ei).to(DEV), model, params,
+                    names, pathways=comms, pathway_names=[f"c{i}" for i in range(4)],
+                    problem="edge_prediction")
+    df, pdf = exp.run("edge_7", times=1)
+    assert pdf is not None and len(pdf) == 4
+    for i, c in enumerate(comms):
+        np.testing.assert_allclose(pdf.loc[f"c{i}", "score"],
+                                   np.mean([df.loc[n, "config_value_mean"] for n in c]), atol=1e-5)
