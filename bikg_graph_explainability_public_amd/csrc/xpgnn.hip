@@ -1781,6 +1781,19 @@ __global__ __launch_bounds__(512) void k_wide_l1m(const WideArgs a) {
   }
 }
 
+// Sum over the 32 lanes of each half of the wave (lanes l and l ^ 32 keep separate sums), on the
+// VALU: quad DPP (xor 1, xor 2), row_ror 4 and 8 inside 16-lane rows, then v_permlane16_swap for
+// the two rows of the half.  Every lane of the half ends with the same total.
+__device__ __forceinline__ float half_wave_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));  // row_ror:4
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+
 // One launch per conv layer of a 2-layer plan, persistent (target += gridDim.x).  Item = one
 // target for all 32 samples of the pass.  Its in-edges of every term (source row, F_0 position,
 // 32-sample keep word) are staged in LDS once; then the 16 lane-groups of 16 lanes own samples
@@ -2058,9 +2071,7 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
         for (int reg = 0; reg < 16; ++reg)
           part[reg] = col < a.f_out ? act_apply(acc[reg] + bv, a.act) * hwc : 0.f;
 #pragma unroll
-        for (int o = 16; o > 0; o >>= 1)
-#pragma unroll
-          for (int reg = 0; reg < 16; ++reg) part[reg] += __shfl_xor(part[reg], o);
+        for (int reg = 0; reg < 16; ++reg) part[reg] = half_wave_sum(part[reg]);
         if (i32 == 0) {  // lanes 0 and 32 hold the 16 sample rows of their half
 #pragma unroll
           for (int reg = 0; reg < 16; ++reg) H0[nb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = part[reg];
@@ -2114,6 +2125,280 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
       cur_w = hd.n_pad;
     }
     if (tid < a.nr) a.out[(a.row0 + tid) * a.n_tgt + t] = cur[tid * a.h_ld + a.out_col];
+  }
+}
+
+// Layer 2 + single-logit head of the wide path, warp-specialised (SAGE / GCN plans with one
+// aggregating term; the c3 shape).  The phase costs of k_wide_tgt<.., true, 0> barely overlap
+// (XPG_WIDE_DBG ablation at c3: gathers alone 10.7 ms, MFMA + head alone 20.5 ms, both 30.4 ms
+// per 32-row pass), so here the two run in different waves of ONE persistent workgroup per CU:
+//   waves 0-3  gather: 16-lane groups own samples g and g + 16 of target t_i and fill A[i & 1];
+//              each group reads its in-edges straight from the CSR (16 per chunk, lane = edge,
+//              the next target's first chunk and keep words prefetched while the current one
+//              gathers), compacts the kept ones with ballots and keeps 8 source rows in flight
+//   waves 4-7  MFMA: column block (wave - 4) of act(A W^T + b) for target t_{i-1} from
+//              A[(i - 1) & 1] (v_mfma_f32_32x32x2_f32, weights streamed from L2 through a
+//              register ring, two accumulation chains), the head dot reduced over the block's
+//              columns into H0[(i - 1) & 1]; wave 4 then finishes target t_{i-2}'s logits
+// One LDS barrier per target (double-buffered A and H0).  Same arithmetic per target as
+// k_wide_tgt (fp32, fixed summation order).
+template <int NFI, int KW, int GW>
+__global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(const WideArgs a) {
+  constexpr int RIF = 8;
+  constexpr bool TWO = GW == 4;  // GW = 4 gather waves: a group owns samples g and g + 16; 8: sample g
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int abuf = 32 * a.a_ld;
+  float* H0 = wsm + 2 * abuf;  // [2][f_out_pad]: head partials per (column block, sample)
+  const int ntgt_wg = a.n_tgt > (int)blockIdx.x ? (a.n_tgt - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int kagg = a.agg1;
+  const int ragg = a.rel[kagg];
+  const int32_t* aptr = a.agg_ptr + (int64_t)ragg * (a.n_tgt + 1);
+  if (wave < GW) {
+    // ------------------------------------------------------------------ gather role
+    const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
+    const int s0 = g, s1 = TWO ? g + 16 : g;
+    const bool v0 = s0 < a.nr, v1 = TWO && s1 < a.nr;
+    const float* base0 = a.src + (int64_t)(v0 ? s0 : 0) * a.w_row;
+    const float* base1 = a.src + (int64_t)(v1 ? s1 : 0) * a.w_row;
+    // prefetched state of the group's next target
+    int pb0 = 0, pb1 = 0, psrc = 0, pu0 = 0, ptf0 = 0, ptp = 0;
+    uint32_t pm = 0u, pmv = 0u;
+    auto prefetch = [&](int tn) {
+      pb0 = aptr[tn];
+      pb1 = aptr[tn + 1];
+      ptf0 = a.tgt_f0[tn];
+      ptp = a.tgt_prev[tn];
+      const int e = pb0 + gl;
+      psrc = e < pb1 ? a.agg_src[e] : 0;
+      pu0 = e < pb1 ? a.agg_f0[e] : 0;
+    };
+    auto prefetch_m = [&]() {
+      pmv = a.mT0[ptf0];
+      pm = pb0 + gl < pb1 ? a.mT0[pu0] : 0u;
+    };
+    if (ntgt_wg > 0) {
+      prefetch(blockIdx.x);
+      prefetch_m();
+    }
+    for (int i = 0; i <= ntgt_wg + 1; ++i) {
+      if (i < ntgt_wg && !(a.dbg & 32)) {  // dbg 32 (diagnostics): no gathers
+        const int t = blockIdx.x + i * gridDim.x;
+        const int b0 = pb0, b1 = pb1, tf0 = ptf0, tp = ptp;
+        int esrc = psrc, eu0 = pu0;
+        uint32_t em = pm;
+        const uint32_t mv = pmv;
+        if (i + 1 < ntgt_wg) prefetch(t + gridDim.x);
+        const bool tk0 = v0 && ((mv >> s0) & 1u), tk1 = v1 && ((mv >> s1) & 1u);
+        float* A = wsm + (i & 1) * abuf;
+        for (int k = 0; k < a.n_terms; ++k) {
+          const int kind = a.kind[k], r = a.rel[k];
+          float self0[NFI], self1[NFI];
+          {
+            const float* p0r = base0 + (int64_t)tp * a.rstride + fo;
+            const float* p1r = base1 + (int64_t)tp * a.rstride + fo;
+#pragma unroll
+            for (int q = 0; q < NFI; ++q) {
+              self0[q] = p0r[q];
+              self1[q] = TWO ? p1r[q] : 0.f;
+            }
+          }
+          float acc0[NFI], acc1[NFI];
+          if (kind == XPG_TERM_ROOT) {
+#pragma unroll
+            for (int q = 0; q < NFI; ++q) {
+              acc0[q] = self0[q];
+              acc1[q] = self1[q];
+            }
+          } else {
+            float dt0 = 1.f, dt1 = 1.f;
+            if (kind == XPG_TERM_GCN) {
+              dt0 = inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + s0]);
+              dt1 = inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + s1]);
+            }
+#pragma unroll
+            for (int q = 0; q < NFI; ++q) acc0[q] = acc1[q] = 0.f;
+            int cnt0 = 0, cnt1 = 0;
+            for (int c0 = b0; c0 < b1; c0 += 16) {
+              if (c0 != b0) {  // chunks past the first (in-degree > 16): loaded in place
+                const int e = c0 + gl;
+                esrc = e < b1 ? a.agg_src[e] : 0;
+                eu0 = e < b1 ? a.agg_f0[e] : 0;
+                em = e < b1 ? a.mT0[eu0] : 0u;
+              }
+              uint32_t m0 = static_cast<uint32_t>(__ballot(tk0 && ((em >> s0) & 1u)) >> lb) & 0xFFFFu;
+              uint32_t m1 = static_cast<uint32_t>(__ballot(tk1 && ((em >> s1) & 1u)) >> lb) & 0xFFFFu;
+              cnt0 += __popc(m0);
+              cnt1 += __popc(m1);
+              while (m0 | m1) {  // group-uniform
+                float rr[RIF][NFI];
+                float c0v[RIF], c1v[RIF];
+#pragma unroll
+                for (int q = 0; q < RIF; ++q) {
+                  int j = -1;
+                  bool first = false;
+                  if (m0) {
+                    j = __builtin_ctz(m0);
+                    m0 &= m0 - 1u;
+                    first = true;
+                  } else if (m1) {
+                    j = __builtin_ctz(m1);
+                    m1 &= m1 - 1u;
+                  }
+                  const int jj = j >= 0 ? j : 0;
+                  const int srow = __shfl(esrc, lb + jj, 64);
+                  const int su0 = __shfl(eu0, lb + jj, 64);
+                  c0v[q] = c1v[q] = 0.f;
+#pragma unroll
+                  for (int x = 0; x < NFI; ++x) rr[q][x] = 0.f;
+                  if (j >= 0) {
+                    const float* sp = (first ? base0 : base1) + (int64_t)srow * a.rstride + fo;
+                    const int sidx = first ? s0 : s1;
+                    const float c = kind == XPG_TERM_GCN
+                                        ? (first ? dt0 : dt1) * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + su0) * 32 + sidx])
+                                        : 1.f;
+                    c0v[q] = first ? c : 0.f;
+                    c1v[q] = first ? 0.f : c;
+#pragma unroll
+                    for (int x = 0; x < NFI / 4; ++x) {
+                      const float4 v = reinterpret_cast<const float4*>(sp)[x];
+                      rr[q][4 * x] = v.x;
+                      rr[q][4 * x + 1] = v.y;
+                      rr[q][4 * x + 2] = v.z;
+                      rr[q][4 * x + 3] = v.w;
+                    }
+                  }
+                }
+#pragma unroll
+                for (int q = 0; q < RIF; ++q)
+#pragma unroll
+                  for (int x = 0; x < NFI; ++x) {
+                    acc0[x] = fmaf(c0v[q], rr[q][x], acc0[x]);
+                    acc1[x] = fmaf(c1v[q], rr[q][x], acc1[x]);
+                  }
+              }
+            }
+            if (kind == XPG_TERM_GCN) {
+#pragma unroll
+              for (int q = 0; q < NFI; ++q) {
+                acc0[q] = fmaf(dt0 * dt0, self0[q], acc0[q]);
+                acc1[q] = fmaf(dt1 * dt1, self1[q], acc1[q]);
+              }
+            } else {  // MEAN: 0 when the target is masked out in the sample
+              const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+              const float inv0 = tk0 ? 1.f / static_cast<float>(max(cnt0 + sm, 1)) : 0.f;
+              const float inv1 = tk1 ? 1.f / static_cast<float>(max(cnt1 + sm, 1)) : 0.f;
+#pragma unroll
+              for (int q = 0; q < NFI; ++q) {
+                acc0[q] = fmaf(static_cast<float>(sm), self0[q], acc0[q]) * inv0;
+                acc1[q] = fmaf(static_cast<float>(sm), self1[q], acc1[q]) * inv1;
+              }
+            }
+          }
+          float* a0p = A + s0 * a.a_ld + k * a.w_row + fo;
+          float* a1p = A + s1 * a.a_ld + k * a.w_row + fo;
+#pragma unroll
+          for (int q = 0; q < NFI; q += 4) {
+            *reinterpret_cast<float4*>(a0p + q) = v0 ? make_float4(acc0[q], acc0[q + 1], acc0[q + 2], acc0[q + 3])
+                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (TWO)
+              *reinterpret_cast<float4*>(a1p + q) = v1 ? make_float4(acc1[q], acc1[q + 1], acc1[q + 2], acc1[q + 3])
+                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+        if (i + 1 < ntgt_wg) prefetch_m();
+      }
+      lds_barrier();
+    }
+  } else {
+    // ------------------------------------------------------------------ MFMA role
+    const int nb = wave - GW, i32 = lane & 31, h = lane >> 5;
+    const bool active = nb * 32 < a.f_out_pad;
+    const int col = nb * 32 + i32;
+    const float bv = active && col < a.f_out ? a.bias[col] : 0.f;
+    const float hwc = active && col < a.f_out ? a.H[0].weight[col] : 0.f;
+    const float hb = a.H[0].bias[0];
+    const float* wp = a.weight + (int64_t)(active ? col : 0) * a.K + 4 * h;
+    const int klast = a.K - 8;
+    auto ldw = [&](int k) { return *reinterpret_cast<const float4*>(wp + (k < klast ? k : klast)); };
+    float4 wreg[KW > 0 ? KW : 1];  // KW > 0: the wave's 32 weight columns held in registers (K = 8 KW)
+    if (KW > 0) {
+#pragma unroll
+      for (int kk = 0; kk < (KW > 0 ? KW : 1); ++kk) wreg[kk] = ldw(kk * 8);
+    }
+    for (int i = 0; i <= ntgt_wg + 1; ++i) {
+      if (nb == 0 && i >= 2 && lane < a.nr) {  // target t_{i-2}: y[s] = act(sum over blocks + b)
+        const float* hp = H0 + (i & 1) * a.f_out_pad;  // written at iteration i - 1 into buffer (i - 2) & 1
+        float v = 0.f;
+        for (int b = 0; b * 32 < a.f_out_pad; ++b) v += hp[b * 32 + lane];
+        const int tf = blockIdx.x + (i - 2) * gridDim.x;
+        a.out[(a.row0 + lane) * a.n_tgt + tf] = act_apply(v + hb, a.H[0].act);
+      }
+      if (i >= 1 && i <= ntgt_wg && active && !(a.dbg & 16)) {  // dbg 16 (diagnostics): no MFMA
+        const float* ap = wsm + ((i - 1) & 1) * abuf + i32 * a.a_ld + 4 * h;
+        auto lda = [&](int k) { return *reinterpret_cast<const float4*>(ap + k); };
+        f32x16 acc, acc2;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = acc2[q] = 0.f;
+        if (KW > 0) {
+#pragma unroll
+          // one accumulation chain (f32 32x32x2: 64-cycle issue = 64-cycle dependent latency)
+          for (int kk = 0; kk < (KW > 0 ? KW : 1); ++kk) {
+            const float4 av = lda(kk * 8);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, wreg[kk].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, wreg[kk].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, wreg[kk].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, wreg[kk].w, acc, 0, 0, 0);
+          }
+        } else {
+        float4 w0 = ldw(0), w1 = ldw(8), w2 = ldw(16), w3 = ldw(24);
+        float4 a0 = lda(0), a1 = lda(8);
+        __builtin_amdgcn_sched_barrier(0);
+        for (int kc = 0; kc < a.K; kc += 32) {
+          const float4 a2 = lda(kc + 16), a3 = lda(kc + 24);
+          __builtin_amdgcn_sched_barrier(0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, w0.x, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, w1.x, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, w0.y, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, w1.y, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, w0.z, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, w1.z, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, w0.w, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, w1.w, acc2, 0, 0, 0);
+          w0 = ldw(kc + 32);
+          w1 = ldw(kc + 40);
+          const int kn = kc + 32 < a.K ? kc + 32 : 0;
+          a0 = lda(kn);
+          a1 = lda(kn + 8);
+          __builtin_amdgcn_sched_barrier(0);  // keep the refills here (the scheduler sinks them to the use)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.x, w2.x, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.x, w3.x, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.y, w2.y, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.y, w3.y, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.z, w2.z, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.z, w3.z, acc2, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.w, w2.w, acc, 0, 0, 0);
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a3.w, w3.w, acc2, 0, 0, 0);
+          w2 = ldw(kc + 48);
+          w3 = ldw(kc + 56);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
+        float part[16];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) part[reg] = col < a.f_out ? act_apply(acc[reg] + bv, a.act) * hwc : 0.f;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) part[reg] = half_wave_sum(part[reg]);
+        if (i32 == 0) {  // lanes 0 and 32 hold the 16 sample rows of their half
+          float* hp = H0 + ((i - 1) & 1) * a.f_out_pad;
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) hp[nb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = part[reg];
+        }
+      }
+      lds_barrier();
+    }
   }
 }
 
@@ -3606,18 +3891,39 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
                                                                  : wide_kernel<false>(l1.f_out_pad / 16, 0);
   void (*k2)(WideArgs) = wide_kernel<true>(l2.f_in_pad / 16, W.kw);
   if (!k1 || !k2) return fail(XPG_EINVAL, "wide forward: unsupported layer width");
+  // warp-specialised layer 2 (gather waves || MFMA waves) for single-logit heads over one
+  // aggregating term (XPG_WIDE_WS=0: the one-role kernel)
+  const char* wse = getenv("XPG_WIDE_WS");
+  const int nfi2 = l2.f_in_pad / 16;
+  const bool ws2 = !(wse && std::strcmp(wse, "0") == 0) && a2.head1 && W.kw == 0 && a2.agg1 >= 0 &&
+                   l2.f_out_pad <= 128 && (nfi2 == 4 || nfi2 == 8) && !(a2.dbg & 15);
+  const size_t lds_ws = sizeof(float) * (size_t)(2 * 32 * W.a_ld + 2 * l2.f_out_pad);
+  // K = 256 (two 128-wide terms: SAGE): the MFMA waves hold their weight columns in registers
+  const char* wsk = getenv("XPG_WIDE_WSKW");
+  const bool kw32 = a2.K == 256 && !(wsk && std::strcmp(wsk, "0") == 0);
+  const char* gwe = getenv("XPG_WIDE_GW");  // gather waves of the specialised kernel: 4 or 8
+  const int gw = gwe && atoi(gwe) == 4 ? 4 : 8;
+  if (ws2) {
+    if (gw == 8) k2 = nfi2 == 8 ? (kw32 ? k_wide_last_ws<8, 32, 8> : k_wide_last_ws<8, 0, 8>)
+                                : (kw32 ? k_wide_last_ws<4, 32, 8> : k_wide_last_ws<4, 0, 8>);
+    else k2 = nfi2 == 8 ? (kw32 ? k_wide_last_ws<8, 32, 4> : k_wide_last_ws<8, 0, 4>)
+                        : (kw32 ? k_wide_last_ws<4, 32, 4> : k_wide_last_ws<4, 0, 4>);
+  }
+  const size_t lds2 = ws2 ? lds_ws : W.lds;
+  const char* gwe0 = getenv("XPG_WIDE_GW");
+  const int thr2 = ws2 ? 64 * ((gwe0 && atoi(gwe0) == 4 ? 4 : 8) + 4) : 256;
   const bool l1m = k1 == k_wide_l1m;
   const size_t lds1 = l1m ? sizeof(float) * 32 * (size_t)(l1.f_out_pad + 4) : sizeof(float) * 3 * kWideCap;
   const int thr1 = l1m ? 512 : 256;
   XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds1)));
   XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(W.lds)));
+                              static_cast<int>(lds2)));
   const int cus = device_cus();
   // persistent grids sized to residency (static target striding: no late starters)
   int per_cu1 = 0, per_cu2 = 0;
   XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu1, reinterpret_cast<const void*>(k1), thr1, lds1));
-  XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, reinterpret_cast<const void*>(k2), 256, W.lds));
+  XPG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, reinterpret_cast<const void*>(k2), thr2, lds2));
   per_cu1 = std::max(1, per_cu1);
   per_cu2 = std::max(1, per_cu2);
   const unsigned g1 = static_cast<unsigned>(std::min<int64_t>(l1.n_tgt, per_cu1 * (int64_t)cus));
@@ -3642,7 +3948,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
     XPG_LAUNCHED();
     a2.nr = nr;
     a2.row0 = r0;
-    hipLaunchKernelGGL(k2, dim3(g2), dim3(256), W.lds, st, a2);
+    hipLaunchKernelGGL(k2, dim3(g2), dim3(thr2), lds2, st, a2);
     XPG_LAUNCHED();
   }
   return XPG_OK;
