@@ -2402,6 +2402,117 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   }
 }
 
+// Layer 1 of the wide path, one wave per target and all 32 samples at once.  Features are never
+// masked (data.py:582), so the table row T[u] of an in-edge is the same for every sample: the
+// wave reads it once (lane = FPL features, 512 B coalesced at F = 128) and adds it to the
+// accumulators of the samples that keep the edge (keep bits wave-uniform: v_readlane of the
+// lane-per-edge keep words), instead of every 16-lane sample group fetching its own copy.
+// Plans whose term 0 aggregates (GCN / MEAN) and whose other terms are ROOT (homogeneous GCN and
+// SAGE layers); rows are fetched 8 edges ahead.  Per sample the edges (CSR order), self terms
+// and ROOT terms are summed in k_wide_tgt's order, so h1 is bitwise the gather kernel's.
+template <int FPL>
+__global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
+  constexpr int RIF = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t valid = a.nr >= 32 ? 0xFFFFFFFFu : ((1u << a.nr) - 1u);
+  const bool gcn = a.kind[0] == XPG_TERM_GCN;
+  const int r = a.rel[0];
+  const float* T = a.table[0] + lane * FPL;
+  const int32_t* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+  for (int64_t t = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); t < a.n_tgt; t += nw) {
+    const int tf0 = a.tgt_f0[t];
+    const uint32_t mv = a.mT0[tf0] & valid;
+    float tot[32][FPL];
+#pragma unroll
+    for (int s = 0; s < 32; ++s)
+#pragma unroll
+      for (int q = 0; q < FPL; ++q) tot[s][q] = 0.f;
+    float self[FPL];
+#pragma unroll
+    for (int q = 0; q < FPL; ++q) self[q] = T[(int64_t)tf0 * a.w_row + q];
+    // lane s (< 32): sample s's GCN target factor dt_s and kept in-edge count
+    const float dt_l = gcn ? inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + (lane & 31)]) : 1.f;
+    int cnt_l = 0;
+    const int b0 = pp[t], b1 = pp[t + 1];
+    for (int c0 = b0; c0 < b1; c0 += 64) {
+      const int e = c0 + lane;
+      const int u0v = e < b1 ? a.agg_f0[e] : 0;
+      const uint32_t kmv = e < b1 ? (a.mT0[u0v] & mv) : 0u;
+      const int ne = min(64, b1 - c0);
+      for (int j0 = 0; j0 < ne; j0 += RIF) {
+        float row[RIF][FPL];
+        float c_l[RIF];
+        uint32_t km[RIF];
+#pragma unroll
+        for (int jj = 0; jj < RIF; ++jj) {  // RIF rows in flight
+          const int j = j0 + jj < ne ? j0 + jj : j0;
+          km[jj] = j0 + jj < ne ? __builtin_amdgcn_readlane(kmv, j) : 0u;
+          const int u0 = __builtin_amdgcn_readlane(u0v, j);
+#pragma unroll
+          for (int q = 0; q < FPL; ++q) row[jj][q] = T[(int64_t)u0 * a.w_row + q];
+          c_l[jj] = gcn ? dt_l * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + u0) * 32 + (lane & 31)]) : 1.f;
+        }
+#pragma unroll
+        for (int jj = 0; jj < RIF; ++jj) {
+          if (km[jj] == 0u) continue;  // wave-uniform
+          cnt_l += (km[jj] >> (lane & 31)) & 1u;
+#pragma unroll
+          for (int s = 0; s < 32; ++s) {
+            if ((km[jj] >> s) & 1u) {  // wave-uniform
+              const float c = gcn ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c_l[jj]), s)) : 1.f;
+#pragma unroll
+              for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(c, row[jj][q], tot[s][q]);
+            }
+          }
+        }
+      }
+    }
+    const int sm = gcn ? 0 : a.self_mult[(int64_t)r * a.n_tgt + t];
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      if (gcn) {
+        const float dt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dt_l), s));
+#pragma unroll
+        for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(dt * dt, self[q], tot[s][q]);
+      } else {
+        const int cnt = __builtin_amdgcn_readlane(cnt_l, s);
+        const float inv = ((mv >> s) & 1u) ? 1.f / static_cast<float>(max(cnt + sm, 1)) : 0.f;
+#pragma unroll
+        for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(static_cast<float>(sm), self[q], tot[s][q]) * inv;
+      }
+    }
+    for (int k = 1; k < a.n_terms; ++k) {  // ROOT terms (host-checked)
+      const float* Tk = a.table[k] + lane * FPL;
+      float sk[FPL];
+#pragma unroll
+      for (int q = 0; q < FPL; ++q) sk[q] = Tk[(int64_t)tf0 * a.w_row + q];
+#pragma unroll
+      for (int s = 0; s < 32; ++s)
+#pragma unroll
+        for (int q = 0; q < FPL; ++q) tot[s][q] += sk[q];
+    }
+    float bv[FPL];
+#pragma unroll
+    for (int q = 0; q < FPL; ++q) bv[q] = lane * FPL + q < a.f_real ? a.bias[lane * FPL + q] : 0.f;
+    float* o = a.out + (int64_t)t * 32 * a.w_row + lane * FPL;
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      if (s < a.nr) {
+        float v[FPL];
+#pragma unroll
+        for (int q = 0; q < FPL; ++q) v[q] = lane * FPL + q < a.f_real ? act_apply(tot[s][q] + bv[q], a.act) : 0.f;
+        if (FPL == 2) {
+          *reinterpret_cast<float2*>(o + s * a.w_row) = make_float2(v[0], v[1]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < FPL; ++q) o[s * a.w_row + q] = v[q];
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------ surrogate
 // train_model (wlm.py:132-278) in three stages:
 //  1. k_wlm_stats  (grid, block per Adam step): per-step constants that do not depend on w —
@@ -3884,11 +3995,20 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   a2.head1 = p->n_head == 1 && p->head[0].n_real == 1 && p->out_col == 0;
   a2.src = h1;
   a2.out = y;
-  // layer 1: the lane-group gather kernel (default, faster on MI355X at c3) or the MFMA formulation
-  // (XPG_WIDE_L1=mfma; kept as the second implementation both parity suites run)
+  // layer 1: one wave per target over all 32 samples, each table row read once (k_wide_l1s,
+  // widths 64 / 128 / 256; default when term 0 aggregates and the others are ROOT), else the
+  // 16-lane-group gather kernel (XPG_WIDE_L1=gather forces it) or the MFMA formulation
+  // (XPG_WIDE_L1=mfma); the parity suites run all three
   const char* l1e = getenv("XPG_WIDE_L1");
   void (*k1)(WideArgs) = (l1e && std::strcmp(l1e, "mfma") == 0) ? k_wide_l1m
                                                                  : wide_kernel<false>(l1.f_out_pad / 16, 0);
+  bool l1s_ok = a1.n_terms >= 1 && a1.kind[0] != XPG_TERM_ROOT;  // term 0 aggregates, the rest ROOT
+  for (int k = 1; k < a1.n_terms; ++k) l1s_ok &= a1.kind[k] == XPG_TERM_ROOT;
+  if ((!l1e || !*l1e) && l1s_ok) {
+    if (l1.f_out_pad == 64) k1 = k_wide_l1s<1>;
+    else if (l1.f_out_pad == 128) k1 = k_wide_l1s<2>;
+    else if (l1.f_out_pad == 256) k1 = k_wide_l1s<4>;
+  }
   void (*k2)(WideArgs) = wide_kernel<true>(l2.f_in_pad / 16, W.kw);
   if (!k1 || !k2) return fail(XPG_EINVAL, "wide forward: unsupported layer width");
   // warp-specialised layer 2 (gather waves || MFMA waves) for single-logit heads over one

@@ -50,8 +50,8 @@ def _force(monkeypatch, path):
     the plan an error instead of a silent fall-back (so the named kernel really ran)."""
     monkeypatch.setenv("XPG_FORWARD", path.split("-")[0])
     monkeypatch.setenv("XPG_FORWARD_STRICT", "1")
-    if path == "wide-mfma":
-        monkeypatch.setenv("XPG_WIDE_L1", "mfma")
+    if path in ("wide-mfma", "wide-gather"):
+        monkeypatch.setenv("XPG_WIDE_L1", path.split("-")[1])
     else:
         monkeypatch.delenv("XPG_WIDE_L1", raising=False)
 
@@ -89,7 +89,7 @@ def _masks(R, S, seed):
 
 
 # ------------------------------------------------------------------ hubs, all targets
-@pytest.mark.parametrize("path", ["wide", "wide-mfma", "unfused"])
+@pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1])])
