@@ -54,6 +54,10 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_L1", path.split("-")[1])
     else:
         monkeypatch.delenv("XPG_WIDE_L1", raising=False)
+    if path == "wide-exact":  # layer 2 on the exact fp32 MFMA instead of three-piece bf16
+        monkeypatch.setenv("XPG_WIDE_B3", "0")
+    else:
+        monkeypatch.delenv("XPG_WIDE_B3", raising=False)
 
 
 def _spec(kind, dims, fc, arch):
@@ -89,7 +93,7 @@ def _masks(R, S, seed):
 
 
 # ------------------------------------------------------------------ hubs, all targets
-@pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "unfused"])
+@pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1])])

@@ -29,17 +29,20 @@ def _eng():
     return engine
 
 
-@pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather"])
+@pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather", "wide-exact"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
     32-samples-per-pass wide path for 2-layer plans (XPG_FORWARD=wide; default for frontiers of
     8192+ nodes) and the multi-kernel path (XPG_FORWARD=unfused, also the fallback for plans the
     others do not take; "wide-mfma" / "wide-gather" = the wide path with its MFMA / 16-lane-group
-    gather layer-1 kernel instead of the default one-wave-per-target k_wide_l1s)."""
+    gather layer-1 kernel instead of the default one-wave-per-target k_wide_l1s; "wide-exact" =
+    layer 2 on the exact fp32 MFMA instead of the three-piece bf16 products)."""
     monkeypatch.setenv("XPG_FORWARD", request.param.split("-")[0])
     if request.param in ("wide-mfma", "wide-gather"):
         monkeypatch.setenv("XPG_WIDE_L1", request.param.split("-")[1])
+    if request.param == "wide-exact":
+        monkeypatch.setenv("XPG_WIDE_B3", "0")
     return request.param
 
 
