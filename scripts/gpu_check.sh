@@ -15,7 +15,7 @@ export PYTHONUNBUFFERED=1
 for step in "$@"; do
   case $step in
     build) run build 300 python -c "import __graft_entry__ as g; g.build()" ;;
-    tests) run gpu_tests 900 python -m pytest tests -m gpu -q -rf ;;
+    tests) run gpu_tests 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py ;;
     bench10) run bench10 600 python bench.py --repeats 10 --no-cpu-baseline ;;
