@@ -2142,21 +2142,51 @@ __global__ __launch_bounds__(256, LAST ? (KW == 0 && NFI <= 8 ? 3 : 2) : (NFI >=
 //              columns into H0[(i - 1) & 1]; wave 4 then finishes target t_{i-2}'s logits
 // One LDS barrier per target (double-buffered A and H0).  Same arithmetic per target as
 // k_wide_tgt (fp32, fixed summation order).
-template <int NFI, int KW, int GW>
+// B3 (K = 256, the c3 SAGE shape): the f32 products run as three bf16 products on
+// v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate per k): the gather waves store each A value
+// as hi = bf16(a), lo = bf16(a - hi) (two bf16 tiles, rows of K + 8 elements: the ds_read_b128
+// lane groups hit 16 distinct 16-B bank quads), the MFMA waves split their weight columns the
+// same way once into registers, and acc += a_hi w_hi + a_hi w_lo + a_lo w_hi (fp32 accumulate).
+// Each operand keeps ~16 significant bits and the dropped a_lo w_lo term is ~2^-16 of the
+// product: relative error ~1e-5 per product, accumulated with random signs (the parity suites
+// run both; XPG_WIDE_B3=0 selects the exact f32 MFMA).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = static_cast<__bf16>(x[j]);
+    lo[j] = static_cast<__bf16>(x[j] - static_cast<float>(hi[j]));
+  }
+}
+
+// TEAMS = 2 (GW = 8): the gather waves form two teams of 4 that gather two different targets
+// at once (a group owns samples g and g + 16 of its team's target), so a CU keeps twice the
+// rows in flight; the MFMA waves then take both targets of the previous interval (four A
+// buffers).  A group's own gather is one dependent chain (CSR -> keep bits -> rows), so more
+// targets in flight, not more waves per target, is what raises the CU's memory parallelism.
+template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1>
 __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(const WideArgs a) {
   constexpr int RIF = 8;
-  constexpr bool TWO = GW == 4;  // GW = 4 gather waves: a group owns samples g and g + 16; 8: sample g
+  // GW / TEAMS = 4 gather waves per target: a group owns samples g and g + 16; 8: sample g
+  constexpr bool TWO = GW / TEAMS == 4;
+  static_assert(TEAMS == 1 || (TEAMS == 2 && GW == 8), "two teams of four gather waves");
+  static_assert(!B3 || (KW == 32 && NFI == 8), "B3: K = 256, 8 features per gather lane");
+  constexpr int KB = B3 ? 8 * KW / 16 : 1;  // bf16 k-blocks of 16
   extern __shared__ __attribute__((aligned(16))) float wsm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int abuf = 32 * a.a_ld;
-  float* H0 = wsm + 2 * abuf;  // [2][f_out_pad]: head partials per (column block, sample)
+  const int aph = a.K + 8;  // B3: bf16 elements per A row
+  const int abuf = B3 ? 32 * aph : 32 * a.a_ld;  // floats per A buffer (B3: hi + lo bf16 tiles)
+  float* H0 = wsm + 2 * TEAMS * abuf;  // [2][TEAMS][f_out_pad]: head partials per (column block, sample)
   const int ntgt_wg = a.n_tgt > (int)blockIdx.x ? (a.n_tgt - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nint = (ntgt_wg + TEAMS - 1) / TEAMS;  // intervals (one LDS barrier each)
   const int kagg = a.agg1;
   const int ragg = a.rel[kagg];
   const int32_t* aptr = a.agg_ptr + (int64_t)ragg * (a.n_tgt + 1);
   if (wave < GW) {
     // ------------------------------------------------------------------ gather role
-    const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
+    const int team = TEAMS == 2 ? wave >> 2 : 0;
+    const int g = (TEAMS == 2 ? tid & 255 : tid) >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
     const int s0 = g, s1 = TWO ? g + 16 : g;
     const bool v0 = s0 < a.nr, v1 = TWO && s1 < a.nr;
     const float* base0 = a.src + (int64_t)(v0 ? s0 : 0) * a.w_row;
@@ -2177,20 +2207,21 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       pmv = a.mT0[ptf0];
       pm = pb0 + gl < pb1 ? a.mT0[pu0] : 0u;
     };
-    if (ntgt_wg > 0) {
-      prefetch(blockIdx.x);
+    if (team < ntgt_wg) {
+      prefetch(blockIdx.x + team * gridDim.x);
       prefetch_m();
     }
-    for (int i = 0; i <= ntgt_wg + 1; ++i) {
-      if (i < ntgt_wg && !(a.dbg & 32)) {  // dbg 32 (diagnostics): no gathers
-        const int t = blockIdx.x + i * gridDim.x;
+    for (int i = 0; i <= nint + 1; ++i) {
+      const int idx = TEAMS * i + team;  // the team's target of this interval
+      if (idx < ntgt_wg && !(a.dbg & 32)) {  // dbg 32 (diagnostics): no gathers
+        const int t = blockIdx.x + idx * gridDim.x;
         const int b0 = pb0, b1 = pb1, tf0 = ptf0, tp = ptp;
         int esrc = psrc, eu0 = pu0;
         uint32_t em = pm;
         const uint32_t mv = pmv;
-        if (i + 1 < ntgt_wg) prefetch(t + gridDim.x);
+        if (idx + TEAMS < ntgt_wg) prefetch(t + TEAMS * gridDim.x);
         const bool tk0 = v0 && ((mv >> s0) & 1u), tk1 = v1 && ((mv >> s1) & 1u);
-        float* A = wsm + (i & 1) * abuf;
+        float* A = wsm + ((i & 1) * TEAMS + team) * abuf;
         for (int k = 0; k < a.n_terms; ++k) {
           const int kind = a.kind[k], r = a.rel[k];
           float self0[NFI], self1[NFI];
@@ -2295,6 +2326,24 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
               }
             }
           }
+          if constexpr (B3) {
+            __bf16* Ah = reinterpret_cast<__bf16*>(A);
+            bf16x8 hi, lo;
+#pragma unroll
+            for (int q = 0; q < NFI; ++q) acc0[q] = v0 ? acc0[q] : 0.f;
+            split_bf16x8(acc0, hi, lo);
+            const int e0 = s0 * aph + k * a.w_row + fo;
+            *reinterpret_cast<bf16x8*>(Ah + e0) = hi;
+            *reinterpret_cast<bf16x8*>(Ah + 32 * aph + e0) = lo;
+            if (TWO) {
+#pragma unroll
+              for (int q = 0; q < NFI; ++q) acc1[q] = v1 ? acc1[q] : 0.f;
+              split_bf16x8(acc1, hi, lo);
+              const int e1 = s1 * aph + k * a.w_row + fo;
+              *reinterpret_cast<bf16x8*>(Ah + e1) = hi;
+              *reinterpret_cast<bf16x8*>(Ah + 32 * aph + e1) = lo;
+            }
+          } else {
           float* a0p = A + s0 * a.a_ld + k * a.w_row + fo;
           float* a1p = A + s1 * a.a_ld + k * a.w_row + fo;
 #pragma unroll
@@ -2305,8 +2354,9 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
               *reinterpret_cast<float4*>(a1p + q) = v1 ? make_float4(acc1[q], acc1[q + 1], acc1[q + 2], acc1[q + 3])
                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
           }
+          }
         }
-        if (i + 1 < ntgt_wg) prefetch_m();
+        if (idx + TEAMS < ntgt_wg) prefetch_m();
       }
       lds_barrier();
     }
@@ -2321,26 +2371,56 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     const float* wp = a.weight + (int64_t)(active ? col : 0) * a.K + 4 * h;
     const int klast = a.K - 8;
     auto ldw = [&](int k) { return *reinterpret_cast<const float4*>(wp + (k < klast ? k : klast)); };
-    float4 wreg[KW > 0 ? KW : 1];  // KW > 0: the wave's 32 weight columns held in registers (K = 8 KW)
-    if (KW > 0) {
+    float4 wreg[KW > 0 && !B3 ? KW : 1];  // KW > 0: the wave's 32 weight columns held in registers (K = 8 KW)
+    bf16x8 whi[KB], wlo[KB];                // B3: the same columns as bf16 hi / lo pieces (k = 16 kb + 8 h + j)
+    if (KW > 0 && !B3) {
 #pragma unroll
       for (int kk = 0; kk < (KW > 0 ? KW : 1); ++kk) wreg[kk] = ldw(kk * 8);
     }
-    for (int i = 0; i <= ntgt_wg + 1; ++i) {
-      if (nb == 0 && i >= 2 && lane < a.nr) {  // target t_{i-2}: y[s] = act(sum over blocks + b)
-        const float* hp = H0 + (i & 1) * a.f_out_pad;  // written at iteration i - 1 into buffer (i - 2) & 1
-        float v = 0.f;
-        for (int b = 0; b * 32 < a.f_out_pad; ++b) v += hp[b * 32 + lane];
-        const int tf = blockIdx.x + (i - 2) * gridDim.x;
-        a.out[(a.row0 + lane) * a.n_tgt + tf] = act_apply(v + hb, a.H[0].act);
+    if constexpr (B3) {
+      const float* wb = a.weight + (int64_t)(active ? col : 0) * a.K + 8 * h;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        float x[8];
+        const float4 u = *reinterpret_cast<const float4*>(wb + 16 * kb);
+        const float4 v = *reinterpret_cast<const float4*>(wb + 16 * kb + 4);
+        x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w;
+        x[4] = v.x; x[5] = v.y; x[6] = v.z; x[7] = v.w;
+        split_bf16x8(x, whi[kb], wlo[kb]);
       }
-      if (i >= 1 && i <= ntgt_wg && active && !(a.dbg & 16)) {  // dbg 16 (diagnostics): no MFMA
-        const float* ap = wsm + ((i - 1) & 1) * abuf + i32 * a.a_ld + 4 * h;
+    }
+    for (int i = 0; i <= nint + 1; ++i) {
+#pragma unroll
+      for (int j = 0; j < TEAMS; ++j) {  // targets of interval i - 2: y[s] = act(sum over blocks + b)
+        const int idx = TEAMS * (i - 2) + j;
+        if (nb == 0 && i >= 2 && idx < ntgt_wg && lane < a.nr) {
+          // written at interval i - 1 into buffer (i - 2) & 1 = i & 1
+          const float* hp = H0 + ((i & 1) * TEAMS + j) * a.f_out_pad;
+          float v = 0.f;
+          for (int b = 0; b * 32 < a.f_out_pad; ++b) v += hp[b * 32 + lane];
+          const int tf = blockIdx.x + idx * gridDim.x;
+          a.out[(a.row0 + lane) * a.n_tgt + tf] = act_apply(v + hb, a.H[0].act);
+        }
+      }
+      for (int j = 0; j < TEAMS; ++j) {
+      const int slot = ((i - 1) & 1) * TEAMS + j;
+      if (i >= 1 && TEAMS * (i - 1) + j < ntgt_wg && active && !(a.dbg & 16)) {  // dbg 16 (diagnostics): no MFMA
+        const float* ap = wsm + slot * abuf + i32 * a.a_ld + 4 * h;
         auto lda = [&](int k) { return *reinterpret_cast<const float4*>(ap + k); };
         f32x16 acc, acc2;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = acc2[q] = 0.f;
-        if (KW > 0) {
+        if constexpr (B3) {
+          const __bf16* ah = reinterpret_cast<const __bf16*>(wsm + slot * abuf) + i32 * aph + 8 * h;
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(ah + 16 * kb);
+            const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(ah + 32 * aph + 16 * kb);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, whi[kb], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, wlo[kb], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, whi[kb], acc, 0, 0, 0);
+          }
+        } else if (KW > 0) {
 #pragma unroll
           // one accumulation chain (f32 32x32x2: 64-cycle issue = 64-cycle dependent latency)
           for (int kk = 0; kk < (KW > 0 ? KW : 1); ++kk) {
@@ -2392,10 +2472,11 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) part[reg] = half_wave_sum(part[reg]);
         if (i32 == 0) {  // lanes 0 and 32 hold the 16 sample rows of their half
-          float* hp = H0 + ((i - 1) & 1) * a.f_out_pad;
+          float* hp = H0 + slot * a.f_out_pad;
 #pragma unroll
           for (int reg = 0; reg < 16; ++reg) hp[nb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = part[reg];
         }
+      }
       }
       lds_barrier();
     }
@@ -4017,16 +4098,24 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const int nfi2 = l2.f_in_pad / 16;
   const bool ws2 = !(wse && std::strcmp(wse, "0") == 0) && a2.head1 && W.kw == 0 && a2.agg1 >= 0 &&
                    l2.f_out_pad <= 128 && (nfi2 == 4 || nfi2 == 8) && !(a2.dbg & 15);
-  const size_t lds_ws = sizeof(float) * (size_t)(2 * 32 * W.a_ld + 2 * l2.f_out_pad);
   // K = 256 (two 128-wide terms: SAGE): the MFMA waves hold their weight columns in registers
   const char* wsk = getenv("XPG_WIDE_WSKW");
   const bool kw32 = a2.K == 256 && !(wsk && std::strcmp(wsk, "0") == 0);
+  // ... and by default run the products as three bf16 MFMAs (XPG_WIDE_B3=0: exact f32 MFMA)
+  const char* b3e = getenv("XPG_WIDE_B3");
+  const bool b3 = kw32 && nfi2 == 8 && !(b3e && std::strcmp(b3e, "0") == 0);
   const char* gwe = getenv("XPG_WIDE_GW");  // gather waves of the specialised kernel: 4 or 8
   const int gw = gwe && atoi(gwe) == 4 ? 4 : 8;
+  // two gather teams (two targets in flight per interval) for the K = 256 register-weight kernels
+  const char* tme = getenv("XPG_WIDE_TEAMS");
+  const int teams = gw == 8 && kw32 && nfi2 == 8 && tme && atoi(tme) == 2 ? 2 : 1;
+  const size_t lds_ws =
+      sizeof(float) * (size_t)teams * (size_t)(2 * (b3 ? 32 * (a2.K + 8) : 32 * W.a_ld) + 2 * l2.f_out_pad);
   if (ws2) {
-    if (gw == 8) k2 = nfi2 == 8 ? (kw32 ? k_wide_last_ws<8, 32, 8> : k_wide_last_ws<8, 0, 8>)
-                                : (kw32 ? k_wide_last_ws<4, 32, 8> : k_wide_last_ws<4, 0, 8>);
-    else k2 = nfi2 == 8 ? (kw32 ? k_wide_last_ws<8, 32, 4> : k_wide_last_ws<8, 0, 4>)
+    if (teams == 2) k2 = b3 ? k_wide_last_ws<8, 32, 8, true, 2> : k_wide_last_ws<8, 32, 8, false, 2>;
+    else if (gw == 8) k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 8, true> : kw32 ? k_wide_last_ws<8, 32, 8> : k_wide_last_ws<8, 0, 8>)
+                                     : (kw32 ? k_wide_last_ws<4, 32, 8> : k_wide_last_ws<4, 0, 8>);
+    else k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 4, true> : kw32 ? k_wide_last_ws<8, 32, 4> : k_wide_last_ws<8, 0, 4>)
                         : (kw32 ? k_wide_last_ws<4, 32, 4> : k_wide_last_ws<4, 0, 4>);
   }
   const size_t lds2 = ws2 ? lds_ws : W.lds;

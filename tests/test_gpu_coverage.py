@@ -58,6 +58,10 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_B3", "0")
     else:
         monkeypatch.delenv("XPG_WIDE_B3", raising=False)
+    if path == "wide-teams":  # layer 2 with two gather teams (two targets per interval)
+        monkeypatch.setenv("XPG_WIDE_TEAMS", "2")
+    else:
+        monkeypatch.delenv("XPG_WIDE_TEAMS", raising=False)
 
 
 def _spec(kind, dims, fc, arch):
@@ -93,7 +97,8 @@ def _masks(R, S, seed):
 
 
 # ------------------------------------------------------------------ hubs, all targets
-@pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "unfused"])
+@pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "wide-teams",
+                                  "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1])])

@@ -1,0 +1,72 @@
+"""Diagnostic (not part of the product): A/B of the wide layer-2 kernel variants on the c3
+full-graph forward (1M nodes / 10M edges, 2-layer SAGE 128, every node a target), one plan,
+one 32-row pass per variant; outputs compared with the exact f32 variant (XPG_WIDE_B3=0).
+
+    python tools/ws_ab.py [--nodes N] [--edges E] [--variants "B3=0;B3=1;B3=1,TEAMS=2"]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bikg_graph_explainability_public_amd import _lib, engine, pipeline  # noqa: E402
+from bikg_graph_explainability_public_amd.nn import ConvStack  # noqa: E402
+
+KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW")
+
+
+def set_env(spec):
+    for k in KEYS:
+        os.environ.pop("XPG_WIDE_" + k, None)
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=")
+        os.environ["XPG_WIDE_" + k] = v
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--nodes", type=int, default=1_000_000)
+    p.add_argument("--edges", type=int, default=10_000_000)
+    p.add_argument("--feat", type=int, default=128)
+    p.add_argument("--rows", type=int, default=32)
+    p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--variants", default="B3=0;B3=1;B3=1,TEAMS=2;B3=0,TEAMS=2")
+    args = p.parse_args()
+    dev = torch.device("cuda", 0)
+    _lib.load()
+    g = torch.Generator().manual_seed(0)
+    N, E, F = args.nodes, args.edges, args.feat
+    feat = torch.randn((N, F), generator=g).to(dev)
+    ei = torch.randint(0, N, (2, E), generator=g).to(dev)
+    torch.manual_seed(0)
+    arch = ConvStack("sage", [F, F, F], [F, 1]).eval().to(dev)
+    t0 = time.time()
+    plan = pipeline.build_plan(arch, feat, ei, list(range(N)))
+    bits = engine.sample_shapley(13, args.rows, N, dev)
+    print(f"plan N={N} E={E} F={F} in {time.time() - t0:.1f}s", flush=True)
+    ref = None
+    for spec in args.variants.split(";"):
+        set_env(spec)
+        y = plan.forward(bits)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(args.reps):
+            y = plan.forward(bits)
+        b.record()
+        torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / args.reps
+        if ref is None:
+            set_env("B3=0")
+            ref = plan.forward(bits).clone()
+            set_env(spec)
+        d = float((y - ref).abs().max())
+        print(f"[{spec:>18s}] {args.rows} rows: {ms:8.3f} ms  max|y - y_exact| = {d:.3e}", flush=True)
+    set_env("")
+
+
+if __name__ == "__main__":
+    main()
