@@ -203,7 +203,7 @@ def wlm_bytes(rows, cols, batch):
     return rows * W * 4 + rows * (4 + 8) + cols * 4 * 6 + 8 * math.ceil(rows / batch)
 
 
-WLM_KERNELS = ("k_wlm_stats", "k_wlm_colbits", "k_wlm_fit_mc", "k_wlm_loss", "k_argmin_first")
+WLM_KERNELS = ("k_wlm_prep", "k_wlm_fit_mc", "k_wlm_loss_best")
 
 
 def headline(args, dev, world, rank):

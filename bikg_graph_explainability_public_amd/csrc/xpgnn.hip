@@ -2178,6 +2178,12 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   const int aph = a.K + 8;  // B3: bf16 elements per A row
   const int abuf = B3 ? 32 * aph : 32 * a.a_ld;  // floats per A buffer (B3: hi + lo bf16 tiles)
   float* H0 = wsm + 2 * TEAMS * abuf;  // [2][TEAMS][f_out_pad]: head partials per (column block, sample)
+  // WL (B3, one team): the weight lo pieces live in LDS ([kb][h][column][8] bf16: a ds_read_b128
+  // lane group reads 16 distinct columns = 16 distinct bank quads), which frees 64 VGPRs of the
+  // MFMA waves for A / weight fragments loaded two k-blocks ahead (with all pieces in registers
+  // every A read waited for its LDS latency right before its MFMA)
+  constexpr bool WL = B3 && TEAMS == 1;
+  __bf16* WLs = reinterpret_cast<__bf16*>(H0 + 2 * TEAMS * a.f_out_pad);
   const int ntgt_wg = a.n_tgt > (int)blockIdx.x ? (a.n_tgt - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int nint = (ntgt_wg + TEAMS - 1) / TEAMS;  // intervals (one LDS barrier each)
   const int kagg = a.agg1;
@@ -2222,18 +2228,18 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         if (idx + TEAMS < ntgt_wg) prefetch(t + TEAMS * gridDim.x);
         const bool tk0 = v0 && ((mv >> s0) & 1u), tk1 = v1 && ((mv >> s1) & 1u);
         float* A = wsm + ((i & 1) * TEAMS + team) * abuf;
+        float self0[NFI], self1[NFI];  // the target's own rows: the same for every term
+        {
+          const float* p0r = base0 + (int64_t)tp * a.rstride + fo;
+          const float* p1r = base1 + (int64_t)tp * a.rstride + fo;
+#pragma unroll
+          for (int q = 0; q < NFI; ++q) {
+            self0[q] = p0r[q];
+            self1[q] = TWO ? p1r[q] : 0.f;
+          }
+        }
         for (int k = 0; k < a.n_terms; ++k) {
           const int kind = a.kind[k], r = a.rel[k];
-          float self0[NFI], self1[NFI];
-          {
-            const float* p0r = base0 + (int64_t)tp * a.rstride + fo;
-            const float* p1r = base1 + (int64_t)tp * a.rstride + fo;
-#pragma unroll
-            for (int q = 0; q < NFI; ++q) {
-              self0[q] = p0r[q];
-              self1[q] = TWO ? p1r[q] : 0.f;
-            }
-          }
           float acc0[NFI], acc1[NFI];
           if (kind == XPG_TERM_ROOT) {
 #pragma unroll
@@ -2372,7 +2378,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     const int klast = a.K - 8;
     auto ldw = [&](int k) { return *reinterpret_cast<const float4*>(wp + (k < klast ? k : klast)); };
     float4 wreg[KW > 0 && !B3 ? KW : 1];  // KW > 0: the wave's 32 weight columns held in registers (K = 8 KW)
-    bf16x8 whi[KB], wlo[KB];                // B3: the same columns as bf16 hi / lo pieces (k = 16 kb + 8 h + j)
+    bf16x8 whi[KB], wlo[WL ? 1 : KB];       // B3: the same columns as bf16 hi / lo pieces (k = 16 kb + 8 h + j)
     if (KW > 0 && !B3) {
 #pragma unroll
       for (int kk = 0; kk < (KW > 0 ? KW : 1); ++kk) wreg[kk] = ldw(kk * 8);
@@ -2386,7 +2392,14 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         const float4 v = *reinterpret_cast<const float4*>(wb + 16 * kb + 4);
         x[0] = u.x; x[1] = u.y; x[2] = u.z; x[3] = u.w;
         x[4] = v.x; x[5] = v.y; x[6] = v.z; x[7] = v.w;
-        split_bf16x8(x, whi[kb], wlo[kb]);
+        if constexpr (WL) {
+          bf16x8 lo;
+          split_bf16x8(x, whi[kb], lo);
+          // each lane reads back only what it wrote: no barrier needed before the first use
+          if (active) *reinterpret_cast<bf16x8*>(WLs + ((int64_t)(2 * kb + h) * a.f_out_pad + col) * 8) = lo;
+        } else {
+          split_bf16x8(x, whi[kb], wlo[WL ? 0 : kb]);
+        }
       }
     }
     for (int i = 0; i <= nint + 1; ++i) {
@@ -2410,14 +2423,36 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         f32x16 acc, acc2;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = acc2[q] = 0.f;
-        if constexpr (B3) {
+        if constexpr (WL) {
+          const __bf16* ah = reinterpret_cast<const __bf16*>(wsm + slot * abuf) + i32 * aph + 8 * h;
+          const __bf16* wl = WLs + ((int64_t)h * a.f_out_pad + col) * 8;
+          const int wstep = 2 * a.f_out_pad * 8;  // bf16 per k-block of the lo pieces
+          bf16x8 A1[3], A2[3], WW[3];             // ring: k-blocks kb, kb + 1, kb + 2
+          auto ld = [&](int kb, int r) {
+            A1[r] = *reinterpret_cast<const bf16x8*>(ah + 16 * kb);
+            A2[r] = *reinterpret_cast<const bf16x8*>(ah + 32 * aph + 16 * kb);
+            WW[r] = *reinterpret_cast<const bf16x8*>(wl + kb * wstep);
+          };
+          ld(0, 0);
+          ld(1, 1);
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            if (kb + 2 < KB) ld(kb + 2, (kb + 2) % 3);
+            __builtin_amdgcn_sched_barrier(0);  // keep the reads two k-blocks ahead of their MFMAs
+            const int r = kb % 3;
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2[r], whi[kb], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[r], WW[r], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[r], whi[kb], acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else if constexpr (B3) {
           const __bf16* ah = reinterpret_cast<const __bf16*>(wsm + slot * abuf) + i32 * aph + 8 * h;
 #pragma unroll
           for (int kb = 0; kb < KB; ++kb) {
             const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(ah + 16 * kb);
             const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(ah + 32 * aph + 16 * kb);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, whi[kb], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, wlo[kb], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, wlo[WL ? 0 : kb], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, whi[kb], acc, 0, 0, 0);
           }
         } else if (KW > 0) {
@@ -2491,19 +2526,21 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
 // Plans whose term 0 aggregates (GCN / MEAN) and whose other terms are ROOT (homogeneous GCN and
 // SAGE layers); rows are fetched 8 edges ahead.  Per sample the edges (CSR order), self terms
 // and ROOT terms are summed in k_wide_tgt's order, so h1 is bitwise the gather kernel's.
-template <int FPL>
+template <int FPL, bool GCN>
 __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
   constexpr int RIF = 8;
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   const uint32_t valid = a.nr >= 32 ? 0xFFFFFFFFu : ((1u << a.nr) - 1u);
-  const bool gcn = a.kind[0] == XPG_TERM_GCN;
   const int r = a.rel[0];
   const float* T = a.table[0] + lane * FPL;
   const int32_t* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+  // every per-target quantity below is wave-uniform and forced into SGPRs (readfirstlane): the
+  // per-sample keep tests are then scalar bit tests + scalar branches (with the values in VGPRs
+  // the compiler emitted an exec-mask branch of ~10 instructions per sample and edge)
   for (int64_t t = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); t < a.n_tgt; t += nw) {
-    const int tf0 = a.tgt_f0[t];
-    const uint32_t mv = a.mT0[tf0] & valid;
+    const int tf0 = __builtin_amdgcn_readfirstlane(a.tgt_f0[t]);
+    const uint32_t mv = __builtin_amdgcn_readfirstlane(a.mT0[tf0]) & valid;
     float tot[32][FPL];
 #pragma unroll
     for (int s = 0; s < 32; ++s)
@@ -2513,9 +2550,9 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
 #pragma unroll
     for (int q = 0; q < FPL; ++q) self[q] = T[(int64_t)tf0 * a.w_row + q];
     // lane s (< 32): sample s's GCN target factor dt_s and kept in-edge count
-    const float dt_l = gcn ? inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + (lane & 31)]) : 1.f;
+    const float dt_l = GCN ? inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + (lane & 31)]) : 1.f;
     int cnt_l = 0;
-    const int b0 = pp[t], b1 = pp[t + 1];
+    const int b0 = __builtin_amdgcn_readfirstlane(pp[t]), b1 = __builtin_amdgcn_readfirstlane(pp[t + 1]);
     for (int c0 = b0; c0 < b1; c0 += 64) {
       const int e = c0 + lane;
       const int u0v = e < b1 ? a.agg_f0[e] : 0;
@@ -2532,27 +2569,36 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
           const int u0 = __builtin_amdgcn_readlane(u0v, j);
 #pragma unroll
           for (int q = 0; q < FPL; ++q) row[jj][q] = T[(int64_t)u0 * a.w_row + q];
-          c_l[jj] = gcn ? dt_l * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + u0) * 32 + (lane & 31)]) : 1.f;
+          c_l[jj] = GCN ? dt_l * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + u0) * 32 + (lane & 31)]) : 1.f;
         }
 #pragma unroll
         for (int jj = 0; jj < RIF; ++jj) {
-          if (km[jj] == 0u) continue;  // wave-uniform
-          cnt_l += (km[jj] >> (lane & 31)) & 1u;
+          const uint32_t k = km[jj];
+          if (k == 0u) continue;  // scalar
+          cnt_l += (k >> (lane & 31)) & 1u;
 #pragma unroll
           for (int s = 0; s < 32; ++s) {
-            if ((km[jj] >> s) & 1u) {  // wave-uniform
-              const float c = gcn ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c_l[jj]), s)) : 1.f;
+            if ((k >> s) & 1u) {  // scalar
+              if (GCN) {
+                const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c_l[jj]), s));
 #pragma unroll
-              for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(c, row[jj][q], tot[s][q]);
+                for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(c, row[jj][q], tot[s][q]);
+              } else {
+                // an empty asm with side effects keeps this a scalar branch: if-converted, every
+                // sample cost 2 adds + 2 selects per edge whether its keep bit was set or not
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(1.f, row[jj][q], tot[s][q]);
+              }
             }
           }
         }
       }
     }
-    const int sm = gcn ? 0 : a.self_mult[(int64_t)r * a.n_tgt + t];
+    const int sm = GCN ? 0 : __builtin_amdgcn_readfirstlane(a.self_mult[(int64_t)r * a.n_tgt + t]);
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
-      if (gcn) {
+      if (GCN) {
         const float dt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dt_l), s));
 #pragma unroll
         for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(dt * dt, self[q], tot[s][q]);
@@ -2605,7 +2651,7 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
 //     nibble of a mask row; tables of g (G[row/4][16]) turn M_b^T g into one lookup per nibble of
 //     a column's row vector; parameters and Adam moments stay in registers (CPT per thread).
 //     The loss (closed form of the reference's [B] - [B,1] broadcast, quirk Q1) is computed
-//     afterwards by k_wlm_loss from the recorded predictions and pre-step weights.
+//     afterwards by k_wlm_loss_best from the recorded predictions and pre-step weights.
 struct WlmStep {
   double ybar, ksum, vy;
   double cg;  // 2 / (B sum k): the per-row gradient factor g_j = k_j cg (p_j - ybar)
@@ -2616,23 +2662,22 @@ struct WlmStep {
 // Also clears the multi-workgroup fit's exchange slots (`clr`, n_clr granules) and error words
 // (`clr32`, n_clr32), so the fit needs no memset launches (plain stores; the kernel boundary
 // makes them visible to the fit).
-__global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
-                                                   const double* __restrict__ kern, int64_t rows,
-                                                   int batch, xpg_wlm_params P, int64_t step0,
-                                                   WlmStep* __restrict__ st, uint64_t* __restrict__ clr,
-                                                   int64_t n_clr, uint32_t* __restrict__ clr32, int n_clr32) {
+// block (t, fit) of a (steps x n_fits) grid; nb / b: block count and this block's index for the
+// slot clearing
+__device__ __forceinline__ void wlm_stats_block(const float* __restrict__ y, const double* __restrict__ kern,
+                                                int64_t rows, int batch, const xpg_wlm_params& P, int64_t step0,
+                                                WlmStep* __restrict__ st, uint64_t* __restrict__ clr, int64_t n_clr,
+                                                uint32_t* __restrict__ clr32, int n_clr32, int64_t t, int64_t fit,
+                                                int64_t steps, int64_t nb, int64_t b) {
   __shared__ double red[16];
-  const int64_t t = blockIdx.x;
-  const int64_t fit = blockIdx.y;
   {
-    const int64_t nb = (int64_t)gridDim.x * gridDim.y, b = fit * gridDim.x + t;
     for (int64_t e = b * blockDim.x + threadIdx.x; e < n_clr; e += nb * blockDim.x) clr[e] = 0;
     if (b == 0)
       for (int e = threadIdx.x; e < n_clr32; e += blockDim.x) clr32[e] = 0u;
   }
   y += fit * rows;
   kern += fit * rows;
-  st += fit * (int64_t)gridDim.x;
+  st += fit * steps;
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
   double sy = 0.0, sk = 0.0;
@@ -2666,14 +2711,22 @@ __global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
   }
 }
 
+__global__ __launch_bounds__(256) void k_wlm_stats(const float* __restrict__ y,
+                                                   const double* __restrict__ kern, int64_t rows,
+                                                   int batch, xpg_wlm_params P, int64_t step0,
+                                                   WlmStep* __restrict__ st, uint64_t* __restrict__ clr,
+                                                   int64_t n_clr, uint32_t* __restrict__ clr32, int n_clr32) {
+  const int64_t nb = (int64_t)gridDim.x * gridDim.y;
+  wlm_stats_block(y, kern, rows, batch, P, step0, st, clr, n_clr, clr32, n_clr32, blockIdx.x, blockIdx.y,
+                  gridDim.x, nb, blockIdx.y * (int64_t)gridDim.x + blockIdx.x);
+}
+
 // colbits[(t * cols + c) * bw + jw] bit b = mask bit (row t*batch + 32*jw + b, column c)
 // Lane = (step t, 32-row block jw, mask word wd), wd fastest: 32 row words read coalesced across
 // the lanes of a block, one in-register 32 x 32 bit transpose, 32 column words stored.
-__global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict__ bits, int64_t rows,
-                                                     int cols, int words, int batch, int bw,
-                                                     int64_t steps, uint32_t* __restrict__ colbits) {
-  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t fit = blockIdx.y;
+__device__ __forceinline__ void wlm_colbits_lane(const uint32_t* __restrict__ bits, int64_t rows, int cols,
+                                                 int words, int batch, int bw, int64_t steps,
+                                                 uint32_t* __restrict__ colbits, int64_t gid, int64_t fit) {
   if (gid >= steps * bw * words) return;
   bits += fit * rows * words;
   colbits += fit * steps * cols * bw;
@@ -2694,6 +2747,25 @@ __global__ __launch_bounds__(256) void k_wlm_colbits(const uint32_t* __restrict_
 #pragma unroll
   for (int b = 0; b < 32; ++b)
     if (wd * 32 + b < cols) dst[(int64_t)b * bw] = x[b];
+}
+
+// The fit's two independent prologues in ONE launch (one kernel boundary less on the
+// latency-bound chain): blocks [0, steps) of each fit row are k_wlm_stats' blocks, the rest
+// k_wlm_colbits' 256-lane blocks.
+__global__ __launch_bounds__(256) void k_wlm_prep(const float* __restrict__ y, const double* __restrict__ kern,
+                                                  const uint32_t* __restrict__ bits, int64_t rows, int cols,
+                                                  int words, int batch, int bw, int64_t steps, xpg_wlm_params P,
+                                                  int64_t step0, WlmStep* __restrict__ st,
+                                                  uint32_t* __restrict__ colbits, uint64_t* __restrict__ clr,
+                                                  int64_t n_clr, uint32_t* __restrict__ clr32, int n_clr32) {
+  const int64_t fit = blockIdx.y;
+  if ((int64_t)blockIdx.x < steps) {
+    wlm_stats_block(y, kern, rows, batch, P, step0, st, clr, n_clr, clr32, n_clr32, blockIdx.x, fit, steps,
+                    steps * gridDim.y, fit * steps + blockIdx.x);
+  } else {
+    const int64_t gid = (blockIdx.x - steps) * (int64_t)blockDim.x + threadIdx.x;
+    wlm_colbits_lane(bits, rows, cols, words, batch, bw, steps, colbits, gid, fit);
+  }
 }
 
 
@@ -3137,12 +3209,17 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
   const int nchunk = (ow * 32 + cw - 1) / cw;  // chunks over the own words (tail columns: w = 0, zero T entries)
   const float l1s = Pm.l1_lambda / static_cast<float>(cols);
 
-  // per-thread staging offsets (fixed for the whole fit)
+  // per-thread staging offsets (fixed for the whole fit).  With batch <= 512 the waves past the
+  // B / poll waves do all the staging (ns stagers, sid < 0: a poll wave), so the next step's
+  // loads are not issued between a poll wave's publish and its poll (the step's critical path)
+  const bool split_stage = nrb <= 8;
+  const int ns = split_stage ? 1024 - 64 * nrb : 1024;
+  const int sid = split_stage ? tid - 64 * nrb : tid;
   int ro[STG], rl[STG], cl[STG];  // rows: global word offset (row * words + word), LDS offset | row << 16
   const int n_r = batch * ow, n_c = ncol * bw;
 #pragma unroll
   for (int q = 0; q < STG; ++q) {
-    const int e = q * 1024 + tid;
+    const int e = sid < 0 ? n_r + n_c : q * ns + sid;
     const int rr = e < n_r ? e / ow : 0, wd = e < n_r ? e - rr * ow : 0;
     ro[q] = rr * words + wd;
     rl[q] = (rr * rp + wd) | (rr << 16);
@@ -3158,24 +3235,24 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     const uint32_t* rs_ = bits + r0_ * words;                                           \
     const uint32_t* cs_ = colbits + (TT) * cols * bw;                                   \
     _Pragma("unroll") for (int q = 0; q < STG; ++q) {                                   \
-      const int e_ = q * 1024 + tid;                                                    \
-      if (e_ < n_r) {                                                                   \
+      const int e_ = q * ns + sid;                                                      \
+      if (sid >= 0 && e_ < n_r) {                                                       \
         const int rr_ = rl[q] >> 16;                                                    \
         sr[q] = rs_[rr_ < B_ ? ro[q] : ro[q] - rr_ * words];                            \
       }                                                                                 \
-      if (e_ < n_c) sv[q] = cs_[e_];                                                    \
+      if (sid >= 0 && e_ < n_c) sv[q] = cs_[e_];                                        \
     }                                                                                   \
-    if (tid < B_) kst = kern[r0_ + tid];                                                \
+    if (sid >= 0 && sid < B_) kst = kern[r0_ + sid];                                    \
   }
 #define XPG_MC_STORE(TT)                                                                \
   {                                                                                     \
     uint32_t* cb_ = Cb + ((TT) & 1) * cbuf;                                             \
     _Pragma("unroll") for (int q = 0; q < STG; ++q) {                                   \
-      const int e_ = q * 1024 + tid;                                                    \
-      if (e_ < n_r) Rb[rl[q] & 0xFFFF] = sr[q];                                         \
-      if (e_ < n_c) cb_[cl[q]] = sv[q];                                                 \
+      const int e_ = q * ns + sid;                                                      \
+      if (sid >= 0 && e_ < n_r) Rb[rl[q] & 0xFFFF] = sr[q];                             \
+      if (sid >= 0 && e_ < n_c) cb_[cl[q]] = sv[q];                                     \
     }                                                                                   \
-    if (tid < batch) kbuf[tid] = kst;                                                   \
+    if (sid >= 0 && sid < batch) kbuf[sid] = kst;                                       \
   }
 
   // own columns: column chunk (wave + 16 c), lane col_lo; the slice-0 lane holds w, m, v
@@ -3386,22 +3463,28 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
 
 
 // loss_t = sum_j k_j (p_j - ybar)^2 / (B sum k) + sum_i (y_i - ybar)^2 / B^2 + l1 * mean|w_t|
-__global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hist,
-                                                  const float* __restrict__ w_hist,
-                                                  const double* __restrict__ kern,
-                                                  const WlmStep* __restrict__ stp, int64_t rows,
-                                                  int cols, int batch, float l1,
-                                                  double* __restrict__ losses) {
+// One launch per fit chain for the losses and the best epoch: block (t, fit) computes loss_t
+// (256 threads, the formula above), publishes it, and the fit's last block to finish (arrival
+// counter, cleared by k_wlm_prep) takes the first argmin over the fit's steps in one wave
+// (k_argmin_first's answer: the lowest step among equal minima, step 0 when none is below +inf).
+// Also hands the multi-workgroup exchange's error word to the caller's status word.
+__global__ __launch_bounds__(256) void k_wlm_loss_best(const float* __restrict__ p_hist,
+                                                       const float* __restrict__ w_hist,
+                                                       const double* __restrict__ kern,
+                                                       const WlmStep* __restrict__ stp, int64_t rows,
+                                                       int cols, int batch, float l1,
+                                                       double* __restrict__ losses, int32_t* __restrict__ best,
+                                                       uint32_t* __restrict__ arrive, const uint32_t* __restrict__ errw,
+                                                       int32_t* __restrict__ status) {
   __shared__ double red[16];
-  const int64_t t = blockIdx.x;
-  {
-    const int64_t f = blockIdx.y, steps = gridDim.x;
-    p_hist += f * rows;
-    w_hist += f * steps * cols;
-    kern += f * rows;
-    stp += f * steps;
-    losses += f * steps;
-  }
+  __shared__ int last_s;
+  const int64_t t = blockIdx.x, f = blockIdx.y, steps = gridDim.x;
+  if (status && f == 0 && t == 0 && threadIdx.x == 0) *status = errw ? static_cast<int32_t>(*errw) : 0;
+  p_hist += f * rows;
+  w_hist += f * steps * cols;
+  kern += f * rows;
+  stp += f * steps;
+  losses += f * steps;
   const int64_t r0 = t * batch;
   const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
   const WlmStep sc = stp[t];
@@ -3415,9 +3498,35 @@ __global__ __launch_bounds__(256) void k_wlm_loss(const float* __restrict__ p_hi
   const double Sa = block_sum_d(sa, red);
   if (threadIdx.x == 0) {
     const float reg = l1 * static_cast<float>(Sa / cols);
-    losses[t] = Tk / (static_cast<double>(B) * sc.ksum) + sc.vy / (static_cast<double>(B) * B) +
-                static_cast<double>(reg);
+    const double loss = Tk / (static_cast<double>(B) * sc.ksum) + sc.vy / (static_cast<double>(B) * B) +
+                        static_cast<double>(reg);
+    __hip_atomic_store(losses + t, loss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t n = __hip_atomic_fetch_add(arrive + f, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last_s = n + 1 == static_cast<uint32_t>(steps);
   }
+  __syncthreads();
+  if (!last_s || threadIdx.x >= 64) return;
+  // the fit's last block: every loss is published (acq_rel counter); one wave scans them
+  const int lane = threadIdx.x;
+  double bv = INFINITY;
+  int64_t bi = -1;
+  for (int64_t i = lane; i < steps; i += 64) {
+    const double v = __hip_atomic_load(losses + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v < bv) {
+      bv = v;
+      bi = i;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double ov = __shfl_xor(bv, off, 64);
+    const int64_t oi = __shfl_xor(bi, off, 64);
+    if (oi >= 0 && (bi < 0 || ov < bv || (ov == bv && oi < bi))) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) best[f] = static_cast<int32_t>(bi < 0 ? 0 : bi);
 }
 
 // -------------------------------------------------------------- surrogate, many-column (grid) fit
@@ -4086,9 +4195,10 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   bool l1s_ok = a1.n_terms >= 1 && a1.kind[0] != XPG_TERM_ROOT;  // term 0 aggregates, the rest ROOT
   for (int k = 1; k < a1.n_terms; ++k) l1s_ok &= a1.kind[k] == XPG_TERM_ROOT;
   if ((!l1e || !*l1e) && l1s_ok) {
-    if (l1.f_out_pad == 64) k1 = k_wide_l1s<1>;
-    else if (l1.f_out_pad == 128) k1 = k_wide_l1s<2>;
-    else if (l1.f_out_pad == 256) k1 = k_wide_l1s<4>;
+    const bool g = a1.kind[0] == XPG_TERM_GCN;
+    if (l1.f_out_pad == 64) k1 = g ? k_wide_l1s<1, true> : k_wide_l1s<1, false>;
+    else if (l1.f_out_pad == 128) k1 = g ? k_wide_l1s<2, true> : k_wide_l1s<2, false>;
+    else if (l1.f_out_pad == 256) k1 = g ? k_wide_l1s<4, true> : k_wide_l1s<4, false>;
   }
   void (*k2)(WideArgs) = wide_kernel<true>(l2.f_in_pad / 16, W.kw);
   if (!k1 || !k2) return fail(XPG_EINVAL, "wide forward: unsupported layer width");
@@ -4110,7 +4220,8 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const char* tme = getenv("XPG_WIDE_TEAMS");
   const int teams = gw == 8 && kw32 && nfi2 == 8 && tme && atoi(tme) == 2 ? 2 : 1;
   const size_t lds_ws =
-      sizeof(float) * (size_t)teams * (size_t)(2 * (b3 ? 32 * (a2.K + 8) : 32 * W.a_ld) + 2 * l2.f_out_pad);
+      sizeof(float) * (size_t)teams * (size_t)(2 * (b3 ? 32 * (a2.K + 8) : 32 * W.a_ld) + 2 * l2.f_out_pad) +
+      (b3 && teams == 1 ? sizeof(uint16_t) * (size_t)a2.K * l2.f_out_pad : 0);  // weight lo pieces (bf16)
   if (ws2) {
     if (teams == 2) k2 = b3 ? k_wide_last_ws<8, 32, 8, true, 2> : k_wide_last_ws<8, 32, 8, false, 2>;
     else if (gw == 8) k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 8, true> : kw32 ? k_wide_last_ws<8, 32, 8> : k_wide_last_ws<8, 0, 8>)
@@ -4681,8 +4792,10 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
     L->xcd = !(xe && std::strcmp(xe, "0") == 0);
     const char* pe = getenv("XPG_MC_P");  // tuning override of the parts per fit
     int P = std::min(kMcMaxP, std::max(2, pe ? atoi(pe) : static_cast<int>(cdiv(words, 3))));
-    // the staged rows / column vectors must fit kMcMaxStage words per thread: more parts if not
-    while (P < kMcMaxP && std::max<int64_t>(batch, 32 * L->bw) * cdiv(words, P) > kMcMaxStage * 1024) ++P;
+    // stagers: the waves past the B / poll waves when batch <= 512 (k_wlm_fit_mc's split_stage)
+    const int64_t nrb = cdiv(batch, 64), ns = nrb <= 8 ? 1024 - 64 * nrb : 1024;
+    // the staged rows / column vectors must fit kMcMaxStage words per stager: more parts if not
+    while (P < kMcMaxP && std::max<int64_t>(batch, 32 * L->bw) * cdiv(words, P) > kMcMaxStage * ns) ++P;
     while (P > 1 && (L->xcd ? cdiv(n_fits, 8) * P > device_cus() / 8 : n_fits * P > device_cus())) --P;
     if (P >= 2) {
       const int wpp = static_cast<int>(cdiv(words, P));
@@ -4706,12 +4819,12 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
         }
       }
       const int64_t stage = std::max<int64_t>(batch * wpp, (int64_t)wpp * 32 * L->bw);
-      int stg = static_cast<int>(cdiv(stage, 1024));
+      int stg = static_cast<int>(cdiv(stage, ns));
       stg = stg <= 1 ? 1 : stg <= 2 ? 2 : 4;
       const size_t lds = sizeof(float) * (size_t)((L->bw * 8 * kTabPitch + 1) & ~int64_t(1)) +
                          sizeof(double) * (size_t)batch + sizeof(float) * (size_t)wpp * 8 * kTabPitch +
                          sizeof(uint32_t) * ((size_t)batch * (wpp | 1) + 2 * (size_t)wpp * 32 * (L->bw | 1));
-      if (nd_best > 0 && lds <= lds_cap && stage <= kMcMaxStage * 1024) {
+      if (nd_best > 0 && lds <= lds_cap && stage <= kMcMaxStage * ns) {
         L->mc = true;
         L->P = P;
         L->wpp = wpp;
@@ -4736,8 +4849,8 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   off += align_up(L->stage ? 0 : F * t_bytes);
   L->xp_off = off;
   off += align_up(L->mc ? F * sizeof(uint64_t) * (2 * L->P * (size_t)batch + L->P) : 0);
-  L->cnt_off = off;
-  off += align_up(sizeof(uint32_t) * (F + 1));
+  L->cnt_off = off;  // [F] (unused) + error word + [F] loss arrival counters
+  off += align_up(sizeof(uint32_t) * (2 * F + 1));
   L->total = off;
   return XPG_OK;
 }
@@ -4812,15 +4925,14 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   const int words = words_of(cols);
   const int ic = static_cast<int>(cols), ib = static_cast<int>(batch);
   const unsigned nf = static_cast<unsigned>(n_fits);
-  // the multi-workgroup fit's exchange slots and error words are cleared by k_wlm_stats
+  // the multi-workgroup fit's exchange slots and error words are cleared by k_wlm_prep
   const int64_t n_xp = L.mc ? n_fits * (2 * L.P * batch + L.P) : 0;
-  hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib,
-                     *params, step0, stp, L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
-                     L.mc ? reinterpret_cast<uint32_t*>(ws + L.cnt_off) : nullptr, L.mc ? static_cast<int>(n_fits + 1) : 0);
-  XPG_LAUNCHED();
+  // one launch: the per-step constants (+ exchange slot clearing) and the column bit vectors
   const int64_t lanes = steps * L.bw * words;
-  hipLaunchKernelGGL(k_wlm_colbits, dim3(static_cast<unsigned>(cdiv(lanes, 256)), nf), dim3(256), 0, st, bits, rows, ic,
-                     words, ib, L.bw, steps, colbits);
+  hipLaunchKernelGGL(k_wlm_prep, dim3(static_cast<unsigned>(steps + cdiv(lanes, 256)), nf), dim3(256), 0, st, y,
+                     kernel, bits, rows, ic, words, ib, L.bw, steps, *params, step0, stp, colbits,
+                     L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
+                     reinterpret_cast<uint32_t*>(ws + L.cnt_off), static_cast<int>(2 * n_fits + 1));
   XPG_LAUNCHED();
   bool launched = false;
   const uint32_t* errw = nullptr;
@@ -4855,7 +4967,7 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
 #undef XPG_WLM_MC
     if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported slice width");
     // the exchange's error word (nonzero: a partner's poll timed out, the weights are invalid)
-    // reaches the caller's status through k_argmin_first
+    // reaches the caller's status through k_wlm_loss_best
     errw = cnt + n_fits;
   }
   const int cpt = static_cast<int>(cdiv(cols, 1024));
@@ -4873,10 +4985,10 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   XPG_WLM(1, false) XPG_WLM(2, false) XPG_WLM(4, false) XPG_WLM(8, false) XPG_WLM(16, false)
 #undef XPG_WLM
   if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported column count");
-  hipLaunchKernelGGL(k_wlm_loss, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, p_hist, w_hist, kernel,
-                     stp, rows, ic, ib, params->l1_lambda, losses);
-  XPG_LAUNCHED();
-  hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch, errw, status);
+  // one launch: every step's loss and the first best epoch (+ the exchange status word)
+  hipLaunchKernelGGL(k_wlm_loss_best, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, p_hist, w_hist,
+                     kernel, stp, rows, ic, ib, params->l1_lambda, losses, best_epoch,
+                     reinterpret_cast<uint32_t*>(ws + L.cnt_off) + n_fits + 1, errw, status);
   XPG_LAUNCHED();
   return XPG_OK;
 }

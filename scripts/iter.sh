@@ -1,0 +1,14 @@
+# one GPU iteration: wide parity tests, layer-2 A/B + ablation, surrogate-fit stamp probe
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_coverage.py -x -q --timeout 200 --timeout-method thread -k "wide or full_graph or hub or c3" > gpurun_out/iter_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/iter_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/ws_ab.py --variants "B3=0;B3=1;B3=1,TEAMS=2;B3=1,DBG=16;B3=1,DBG=32" > gpurun_out/iter_ab.log 2>&1; rc=$?
+cat gpurun_out/iter_ab.log
+[ $rc -eq 0 ] || exit $rc
+if [ -x tools/wlm_probe ]; then
+  timeout -k 5 60 ./tools/wlm_probe 1193 12800 256 > gpurun_out/iter_probe.log 2>&1; rc=$?
+  tail -10 gpurun_out/iter_probe.log
+fi
+exit $rc
