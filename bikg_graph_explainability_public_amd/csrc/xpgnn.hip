@@ -1454,7 +1454,8 @@ struct WideArgs {
   int agg1;  // the only aggregating (non-ROOT) term, or -1 when there are several
   int64_t rstride;  // floats between consecutive source rows: w_row (tables) or 32 w_row (h1)
   int head1;  // the head is one Linear(f_out, 1) (+ act) read at column 0: fused epilogue
-  int dbg;   // diagnostics (XPG_WIDE_DBG): 1 skip dense + head, 2 skip row gathers, 4 head, 8 dense
+  int dbg;   // diagnostics (XPG_WIDE_DBG): 1 skip dense + head, 2 skip row gathers, 4 head, 8 dense;
+             // warp-specialised layer 2: 16 no MFMA, 32 no gathers, 64 no epilogue, 128 no products
   int K, a_ld, f_out, f_out_pad, n_head, out_col, h_ld, o_h0, o_h1, o_e;
   int o_hw[kFusedMaxHead];
   const uint32_t* mT0;
@@ -2165,7 +2166,16 @@ __device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8&
 // rows in flight; the MFMA waves then take both targets of the previous interval (four A
 // buffers).  A group's own gather is one dependent chain (CSR -> keep bits -> rows), so more
 // targets in flight, not more waves per target, is what raises the CU's memory parallelism.
-template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1>
+// PIPE (B3 with one team, SAGE-shaped plans: one MEAN term + one ROOT term): the gather role is
+// software-pipelined across its targets.  A group's gather of one target is a chain of four
+// dependent loads (CSR range → edge list → keep words → kept rows), so each stage runs one
+// interval ahead of the next: at the start of interval k the group issues the keep words of
+// target k + 1, the edge list of k + 2 and the CSR range of k + 3; before the barrier of
+// interval k it issues the first 4 kept rows (and the own row) of target k + 1.  Interval k then
+// only consumes loads that were in flight during the previous interval; kept edges past the
+// first 4 of the first 16-edge chunk, and chunks past the first, are gathered in place.
+// Same summation order as the plain gather (bitwise the same A tile).
+template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false>
 __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(const WideArgs a) {
   constexpr int RIF = 8;
   // GW / TEAMS = 4 gather waves per target: a group owns samples g and g + 16; 8: sample g
@@ -2189,7 +2199,168 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   const int kagg = a.agg1;
   const int ragg = a.rel[kagg];
   const int32_t* aptr = a.agg_ptr + (int64_t)ragg * (a.n_tgt + 1);
-  if (wave < GW) {
+  if constexpr (PIPE) {
+    static_assert(!TWO && TEAMS == 1 && B3, "pipelined gather: one sample per group, one team, B3 tiles");
+  }
+  if (PIPE && wave < GW) {
+    // ------------------------------------------------------------------ pipelined gather role
+    const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
+    const int s0 = g;
+    const bool v0 = s0 < a.nr;
+    const float* base0 = a.src + (int64_t)(v0 ? s0 : 0) * a.w_row;
+    const int32_t* smul = a.self_mult + (int64_t)ragg * a.n_tgt;
+    const int kroot = 1 - kagg;  // host-checked: terms {MEAN, ROOT}
+    constexpr int RP = 4;        // prefetched kept rows per target (~2.5 kept per 16-edge chunk)
+    constexpr int RI = 4;        // rows per round of the in-place remainder
+    __bf16* const Ab = reinterpret_cast<__bf16*>(wsm);
+    // stage states: 1 = CSR range / node / prev position / self count, 2 = + this lane's edge,
+    // 3 = + keep words, 4 = + the first kept rows and the own row (the current target)
+    int q1_b0 = 0, q1_b1 = 0, q1_tf0 = 0, q1_tp = 0, q1_sm = 0;
+    int q2_b0 = 0, q2_b1 = 0, q2_tf0 = 0, q2_tp = 0, q2_sm = 0, q2_src = 0, q2_u0 = 0;
+    int q3_b0 = 0, q3_b1 = 0, q3_tp = 0, q3_sm = 0, q3_src = 0, q3_u0 = 0;
+    uint32_t q3_mv = 0u, q3_em = 0u;
+    int q4_b0 = 0, q4_b1 = 0, q4_sm = 0, q4_src = 0, q4_cnt = 0;
+    uint32_t q4_rest = 0u;
+    bool q4_tk = false;
+    float q4_cv[RP], q4_row[RP][NFI], q4_self[NFI];
+    auto st1 = [&](int k) {
+      if (k >= ntgt_wg) return;
+      const int t = blockIdx.x + k * gridDim.x;
+      q1_b0 = aptr[t];
+      q1_b1 = aptr[t + 1];
+      q1_tf0 = a.tgt_f0[t];
+      q1_tp = a.tgt_prev[t];
+      q1_sm = smul[t];
+    };
+    auto st2 = [&](int k) {
+      if (k >= ntgt_wg) return;
+      q2_b0 = q1_b0; q2_b1 = q1_b1; q2_tf0 = q1_tf0; q2_tp = q1_tp; q2_sm = q1_sm;
+      const int e = q1_b0 + gl;
+      q2_src = e < q1_b1 ? a.agg_src[e] : 0;
+      q2_u0 = e < q1_b1 ? a.agg_f0[e] : 0;
+    };
+    auto st3 = [&](int k) {
+      if (k >= ntgt_wg) return;
+      q3_b0 = q2_b0; q3_b1 = q2_b1; q3_tp = q2_tp; q3_sm = q2_sm; q3_src = q2_src; q3_u0 = q2_u0;
+      q3_mv = a.mT0[q2_tf0];
+      q3_em = q2_b0 + gl < q2_b1 ? a.mT0[q2_u0] : 0u;
+    };
+    auto st4 = [&](int k) {  // wave-uniform k: the ballot sees every lane
+      if (k >= ntgt_wg) return;
+      q4_b0 = q3_b0; q4_b1 = q3_b1; q4_sm = q3_sm; q4_src = q3_src;
+      q4_tk = v0 && ((q3_mv >> s0) & 1u);
+      uint32_t m0 = static_cast<uint32_t>(__ballot(q4_tk && ((q3_em >> s0) & 1u)) >> lb) & 0xFFFFu;
+      q4_cnt = __popc(m0);
+#pragma unroll
+      for (int jj = 0; jj < RP; ++jj) {
+        const int j = m0 ? __builtin_ctz(m0) : 0;
+        q4_cv[jj] = m0 ? 1.f : 0.f;
+        m0 &= m0 - 1u;
+        const int srow = __shfl(q3_src, lb + j, 64);
+        const float* sp = base0 + (int64_t)(q4_cv[jj] != 0.f ? srow : q3_tp) * a.rstride + fo;
+#pragma unroll
+        for (int x = 0; x < NFI / 4; ++x) {
+          const float4 v = reinterpret_cast<const float4*>(sp)[x];
+          q4_row[jj][4 * x] = v.x;
+          q4_row[jj][4 * x + 1] = v.y;
+          q4_row[jj][4 * x + 2] = v.z;
+          q4_row[jj][4 * x + 3] = v.w;
+        }
+      }
+      q4_rest = m0;
+      const float* p0r = base0 + (int64_t)q3_tp * a.rstride + fo;
+#pragma unroll
+      for (int x = 0; x < NFI / 4; ++x) {
+        const float4 v = reinterpret_cast<const float4*>(p0r)[x];
+        q4_self[4 * x] = v.x;
+        q4_self[4 * x + 1] = v.y;
+        q4_self[4 * x + 2] = v.z;
+        q4_self[4 * x + 3] = v.w;
+      }
+    };
+    // kept edges of mask m (group lanes = the chunk's edges, sources in esrc) in place, RI rows
+    // per round, added in ctz order
+    auto gather_in_place = [&](uint32_t m, int esrc, float (&acc)[NFI]) {
+      while (m) {  // group-uniform
+        float rr[RI][NFI];
+        float cv[RI];
+#pragma unroll
+        for (int q = 0; q < RI; ++q) {
+          const int j = m ? __builtin_ctz(m) : 0;
+          cv[q] = m ? 1.f : 0.f;
+          m &= m - 1u;
+          const int srow = __shfl(esrc, lb + j, 64);
+          const float* sp = base0 + (int64_t)srow * a.rstride + fo;
+#pragma unroll
+          for (int x = 0; x < NFI / 4; ++x) {
+            const float4 v = reinterpret_cast<const float4*>(sp)[x];
+            rr[q][4 * x] = v.x;
+            rr[q][4 * x + 1] = v.y;
+            rr[q][4 * x + 2] = v.z;
+            rr[q][4 * x + 3] = v.w;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < RI; ++q)
+#pragma unroll
+          for (int x = 0; x < NFI; ++x) acc[x] = fmaf(cv[q], rr[q][x], acc[x]);
+      }
+    };
+    const bool run = !(a.dbg & 32);  // dbg 32 (diagnostics): no gathers
+    if (run) {
+      st1(0); st2(0); st3(0); st4(0);
+      st1(1); st2(1); st1(2);
+    }
+    for (int i = 0; i <= nint + 1; ++i) {
+      if (run && i < ntgt_wg) {
+        st3(i + 1);  // q2 = stage 2 of i + 1 (issued one interval ago)
+        st2(i + 2);  // q1 = stage 1 of i + 2
+        st1(i + 3);
+        float acc[NFI];
+#pragma unroll
+        for (int x = 0; x < NFI; ++x) acc[x] = 0.f;
+#pragma unroll
+        for (int q = 0; q < RP; ++q)
+#pragma unroll
+          for (int x = 0; x < NFI; ++x) acc[x] = fmaf(q4_cv[q], q4_row[q][x], acc[x]);
+        gather_in_place(q4_rest, q4_src, acc);
+        int cnt = q4_cnt;
+        for (int c0 = q4_b0 + 16; c0 < q4_b1; c0 += 16) {  // in-degree > 16: later chunks in place
+          const int e = c0 + gl;
+          const int esrc = e < q4_b1 ? a.agg_src[e] : 0;
+          const int eu0 = e < q4_b1 ? a.agg_f0[e] : 0;
+          const uint32_t em = e < q4_b1 ? a.mT0[eu0] : 0u;
+          const uint32_t m = static_cast<uint32_t>(__ballot(q4_tk && ((em >> s0) & 1u)) >> lb) & 0xFFFFu;
+          cnt += __popc(m);
+          gather_in_place(m, esrc, acc);
+        }
+        const float inv = q4_tk ? 1.f / static_cast<float>(max(cnt + q4_sm, 1)) : 0.f;
+        float self[NFI];
+#pragma unroll
+        for (int x = 0; x < NFI; ++x) {
+          self[x] = q4_self[x];
+          acc[x] = fmaf(static_cast<float>(q4_sm), self[x], acc[x]) * inv;
+        }
+        __bf16* A = Ab + (i & 1) * 2 * abuf;  // abuf floats = 2 abuf bf16
+        bf16x8 hi, lo;
+#pragma unroll
+        for (int x = 0; x < NFI; ++x) {
+          acc[x] = v0 ? acc[x] : 0.f;
+          self[x] = v0 ? self[x] : 0.f;
+        }
+        split_bf16x8(acc, hi, lo);
+        const int ea = s0 * aph + kagg * a.w_row + fo;
+        *reinterpret_cast<bf16x8*>(A + ea) = hi;
+        *reinterpret_cast<bf16x8*>(A + 32 * aph + ea) = lo;
+        split_bf16x8(self, hi, lo);
+        const int er = s0 * aph + kroot * a.w_row + fo;
+        *reinterpret_cast<bf16x8*>(A + er) = hi;
+        *reinterpret_cast<bf16x8*>(A + 32 * aph + er) = lo;
+        st4(i + 1);  // q3 = stage 3 of i + 1 (issued at the top of this interval)
+      }
+      lds_barrier();
+    }
+  } else if (wave < GW) {
     // ------------------------------------------------------------------ gather role
     const int team = TEAMS == 2 ? wave >> 2 : 0;
     const int g = (TEAMS == 2 ? tid & 255 : tid) >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
@@ -2423,7 +2594,8 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         f32x16 acc, acc2;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = acc2[q] = 0.f;
-        if constexpr (WL) {
+        if (a.dbg & 128) {  // dbg 128 (diagnostics): epilogue only, no products
+        } else if constexpr (WL) {
           const __bf16* ah = reinterpret_cast<const __bf16*>(wsm + slot * abuf) + i32 * aph + 8 * h;
           const __bf16* wl = WLs + ((int64_t)h * a.f_out_pad + col) * 8;
           const int wstep = 2 * a.f_out_pad * 8;  // bf16 per k-block of the lo pieces
@@ -2502,10 +2674,23 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
         float part[16];
+        if (a.dbg & 64) {  // dbg 64 (diagnostics): products only, no activation / head reduction
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) part[reg] = col < a.f_out ? act_apply(acc[reg] + bv, a.act) * hwc : 0.f;
+          for (int reg = 0; reg < 16; ++reg) part[reg] = acc[reg];
+        } else {
+          // one scalar branch on the activation for all 16 values (per value, the runtime switch
+          // and the column test were exec-mask branches: the epilogue cost more than the
+          // products); padded columns hold hwc = 0 and zero weights, so they add 0
+          if (a.act == XPG_ACT_RELU) {
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) part[reg] = half_wave_sum(part[reg]);
+            for (int reg = 0; reg < 16; ++reg) part[reg] = fmaxf(acc[reg] + bv, 0.f) * hwc;
+          } else {
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) part[reg] = act_apply(acc[reg] + bv, a.act) * hwc;
+          }
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) part[reg] = half_wave_sum(part[reg]);
+        }
         if (i32 == 0) {  // lanes 0 and 32 hold the 16 sample rows of their half
           float* hp = H0 + slot * a.f_out_pad;
 #pragma unroll
@@ -2537,26 +2722,83 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
   const int32_t* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
   // every per-target quantity below is wave-uniform and forced into SGPRs (readfirstlane): the
   // per-sample keep tests are then scalar bit tests + scalar branches (with the values in VGPRs
-  // the compiler emitted an exec-mask branch of ~10 instructions per sample and edge)
-  for (int64_t t = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); t < a.n_tgt; t += nw) {
-    const int tf0 = __builtin_amdgcn_readfirstlane(a.tgt_f0[t]);
-    const uint32_t mv = __builtin_amdgcn_readfirstlane(a.mT0[tf0]) & valid;
+  // the compiler emitted an exec-mask branch of ~10 instructions per sample and edge).
+  // Cross-target pipeline, three levels deep (vector memory ops complete in issue order, so a
+  // load issued after this target's 32 row stores would first wait for every store's ack):
+  //   A (target t + 2): CSR range and node                      issued at the top of t
+  //   B (target t + 1): first edge chunk, keep word, own row    issued at the top of t (A(t+1) ready)
+  //   C (target t + 1): first chunk's keep words, first 8 rows  issued before t's stores (B ready)
+  int64_t t = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  int a_tf0 = 0, a_b0 = 0, a_b1 = 0;         // A state (lane copies of uniform values)
+  int b_tf0 = 0, b_b0 = 0, b_b1 = 0, b_u0v = 0;  // B state
+  uint32_t b_mv = 0u;
+  float b_self[FPL];
+  uint32_t c_kmv = 0u;                       // C state
+  float c_row[RIF][FPL];
+#pragma unroll
+  for (int q = 0; q < FPL; ++q) b_self[q] = 0.f;
+  auto issueA = [&](int64_t tn) {
+    a_tf0 = a.tgt_f0[tn];
+    a_b0 = pp[tn];
+    a_b1 = pp[tn + 1];
+  };
+  auto issueB = [&]() {  // from A
+    b_tf0 = a_tf0;
+    b_b0 = a_b0;
+    b_b1 = a_b1;
+    const int e = b_b0 + lane;
+    b_u0v = e < b_b1 ? a.agg_f0[e] : 0;
+    b_mv = a.mT0[b_tf0];
+#pragma unroll
+    for (int q = 0; q < FPL; ++q) b_self[q] = T[(int64_t)b_tf0 * a.w_row + q];
+  };
+  auto issueC = [&]() {  // from B
+    const int e = b_b0 + lane;
+    c_kmv = e < b_b1 ? a.mT0[b_u0v] : 0u;
+    const int ne = min(min(64, b_b1 - b_b0), RIF);
+#pragma unroll
+    for (int jj = 0; jj < RIF; ++jj) {
+      const int u0 = __builtin_amdgcn_readlane(b_u0v, jj < ne ? jj : 0);
+#pragma unroll
+      for (int q = 0; q < FPL; ++q) c_row[jj][q] = T[(int64_t)u0 * a.w_row + q];
+    }
+  };
+  if (t < a.n_tgt) {
+    issueA(t);
+    issueB();
+    issueC();
+    if (t + nw < a.n_tgt) issueA(t + nw);
+  }
+  for (; t < a.n_tgt; t += nw) {
+    const int tf0 = __builtin_amdgcn_readfirstlane(b_tf0);
+    const uint32_t mv = __builtin_amdgcn_readfirstlane(b_mv) & valid;
+    const int b0 = __builtin_amdgcn_readfirstlane(b_b0), b1 = __builtin_amdgcn_readfirstlane(b_b1);
+    const int u0v_first = b_u0v;
+    const uint32_t kmv_first = c_kmv & mv;
+    float row0[RIF][FPL];
+#pragma unroll
+    for (int jj = 0; jj < RIF; ++jj)
+#pragma unroll
+      for (int q = 0; q < FPL; ++q) row0[jj][q] = c_row[jj][q];
+    float self[FPL];
+#pragma unroll
+    for (int q = 0; q < FPL; ++q) self[q] = b_self[q];
+    const bool more = t + nw < a.n_tgt;
+    if (more) issueB();                          // target t + nw (A issued one iteration ago)
+    if (t + 2 * nw < a.n_tgt) issueA(t + 2 * nw);
     float tot[32][FPL];
 #pragma unroll
     for (int s = 0; s < 32; ++s)
 #pragma unroll
       for (int q = 0; q < FPL; ++q) tot[s][q] = 0.f;
-    float self[FPL];
-#pragma unroll
-    for (int q = 0; q < FPL; ++q) self[q] = T[(int64_t)tf0 * a.w_row + q];
     // lane s (< 32): sample s's GCN target factor dt_s and kept in-edge count
     const float dt_l = GCN ? inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + tf0) * 32 + (lane & 31)]) : 1.f;
     int cnt_l = 0;
-    const int b0 = __builtin_amdgcn_readfirstlane(pp[t]), b1 = __builtin_amdgcn_readfirstlane(pp[t + 1]);
     for (int c0 = b0; c0 < b1; c0 += 64) {
       const int e = c0 + lane;
-      const int u0v = e < b1 ? a.agg_f0[e] : 0;
-      const uint32_t kmv = e < b1 ? (a.mT0[u0v] & mv) : 0u;
+      const bool first = c0 == b0;
+      const int u0v = first ? u0v_first : (e < b1 ? a.agg_f0[e] : 0);
+      const uint32_t kmv = first ? kmv_first : (e < b1 ? (a.mT0[u0v] & mv) : 0u);
       const int ne = min(64, b1 - c0);
       for (int j0 = 0; j0 < ne; j0 += RIF) {
         float row[RIF][FPL];
@@ -2567,8 +2809,13 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
           const int j = j0 + jj < ne ? j0 + jj : j0;
           km[jj] = j0 + jj < ne ? __builtin_amdgcn_readlane(kmv, j) : 0u;
           const int u0 = __builtin_amdgcn_readlane(u0v, j);
+          if (first && j0 == 0) {  // scalar: the rows prefetched before the previous stores
 #pragma unroll
-          for (int q = 0; q < FPL; ++q) row[jj][q] = T[(int64_t)u0 * a.w_row + q];
+            for (int q = 0; q < FPL; ++q) row[jj][q] = row0[jj][q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < FPL; ++q) row[jj][q] = T[(int64_t)u0 * a.w_row + q];
+          }
           c_l[jj] = GCN ? dt_l * inv_sqrt_deg(a.kinT[((int64_t)r * a.n0 + u0) * 32 + (lane & 31)]) : 1.f;
         }
 #pragma unroll
@@ -2622,6 +2869,7 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
     float bv[FPL];
 #pragma unroll
     for (int q = 0; q < FPL; ++q) bv[q] = lane * FPL + q < a.f_real ? a.bias[lane * FPL + q] : 0.f;
+    if (more) issueC();  // before the stores (see above)
     float* o = a.out + (int64_t)t * 32 * a.w_row + lane * FPL;
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
@@ -4222,8 +4470,14 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const size_t lds_ws =
       sizeof(float) * (size_t)teams * (size_t)(2 * (b3 ? 32 * (a2.K + 8) : 32 * W.a_ld) + 2 * l2.f_out_pad) +
       (b3 && teams == 1 ? sizeof(uint16_t) * (size_t)a2.K * l2.f_out_pad : 0);  // weight lo pieces (bf16)
+  // pipelined gather for the B3 kernel when the plan is SAGE-shaped ({MEAN, ROOT})
+  const char* ppe = getenv("XPG_WIDE_PIPE");
+  const bool pipe = b3 && teams == 1 && gw == 8 && a2.n_terms == 2 && a2.agg1 >= 0 &&
+                    a2.kind[a2.agg1] == XPG_TERM_MEAN && a2.kind[1 - a2.agg1] == XPG_TERM_ROOT &&
+                    !(ppe && std::strcmp(ppe, "0") == 0);
   if (ws2) {
-    if (teams == 2) k2 = b3 ? k_wide_last_ws<8, 32, 8, true, 2> : k_wide_last_ws<8, 32, 8, false, 2>;
+    if (pipe) k2 = k_wide_last_ws<8, 32, 8, true, 1, true>;
+    else if (teams == 2) k2 = b3 ? k_wide_last_ws<8, 32, 8, true, 2> : k_wide_last_ws<8, 32, 8, false, 2>;
     else if (gw == 8) k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 8, true> : kw32 ? k_wide_last_ws<8, 32, 8> : k_wide_last_ws<8, 0, 8>)
                                      : (kw32 ? k_wide_last_ws<4, 32, 8> : k_wide_last_ws<4, 0, 8>);
     else k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 4, true> : kw32 ? k_wide_last_ws<8, 32, 4> : k_wide_last_ws<8, 0, 4>)

@@ -62,6 +62,10 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_TEAMS", "2")
     else:
         monkeypatch.delenv("XPG_WIDE_TEAMS", raising=False)
+    if path == "wide-nopipe":  # B3 layer 2 without the cross-target pipelined gather
+        monkeypatch.setenv("XPG_WIDE_PIPE", "0")
+    else:
+        monkeypatch.delenv("XPG_WIDE_PIPE", raising=False)
 
 
 def _spec(kind, dims, fc, arch):
@@ -98,7 +102,7 @@ def _masks(R, S, seed):
 
 # ------------------------------------------------------------------ hubs, all targets
 @pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "wide-teams",
-                                  "unfused"])
+                                  "wide-nopipe", "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1])])

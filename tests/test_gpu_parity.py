@@ -30,7 +30,7 @@ def _eng():
 
 
 @pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather", "wide-exact",
-                        "wide-teams"])
+                        "wide-teams", "wide-nopipe"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
@@ -39,7 +39,8 @@ def fwd_path(request, monkeypatch):
     others do not take; "wide-mfma" / "wide-gather" = the wide path with its MFMA / 16-lane-group
     gather layer-1 kernel instead of the default one-wave-per-target k_wide_l1s; "wide-exact" =
     layer 2 on the exact fp32 MFMA instead of the three-piece bf16 products; "wide-teams" = the
-    layer-2 kernel with two gather teams, two targets in flight per interval)."""
+    layer-2 kernel with two gather teams, two targets in flight per interval; "wide-nopipe" = the
+    B3 layer-2 kernel without the cross-target pipelined gather)."""
     monkeypatch.setenv("XPG_FORWARD", request.param.split("-")[0])
     if request.param in ("wide-mfma", "wide-gather"):
         monkeypatch.setenv("XPG_WIDE_L1", request.param.split("-")[1])
@@ -47,6 +48,8 @@ def fwd_path(request, monkeypatch):
         monkeypatch.setenv("XPG_WIDE_B3", "0")
     if request.param == "wide-teams":
         monkeypatch.setenv("XPG_WIDE_TEAMS", "2")
+    if request.param == "wide-nopipe":
+        monkeypatch.setenv("XPG_WIDE_PIPE", "0")
     return request.param
 
 
