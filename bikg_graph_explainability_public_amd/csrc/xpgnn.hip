@@ -3569,14 +3569,25 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     if (wave < nrb) {
       if (j < B) {
         const uint32_t* row = Rb + j * rp;
-        for (int kw = 0; kw < ow; kw += 2) {  // 16 lookups in flight (lgkmcnt limit 15)
-          uint32_t wv[2];
+        if (ow <= 4) {  // the usual 3 words per part: all row words, then all lookups (2 LDS round trips)
+          uint32_t wv[4];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) wv[h] = row[kw + h < ow ? kw + h : kw];
+          for (int h = 0; h < 4; ++h) wv[h] = row[h < ow ? h : 0];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const float x = nib8(T + ((kw + h < ow ? kw + h : kw) * 8) * kTabPitch, wv[h]);
-            pown += kw + h < ow ? x : 0.f;
+          for (int h = 0; h < 4; ++h) {
+            const float x = nib8(T + ((h < ow ? h : 0) * 8) * kTabPitch, wv[h]);
+            pown += h < ow ? x : 0.f;
+          }
+        } else {
+          for (int kw = 0; kw < ow; kw += 2) {  // 16 lookups in flight (lgkmcnt limit 15)
+            uint32_t wv[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) wv[h] = row[kw + h < ow ? kw + h : kw];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const float x = nib8(T + ((kw + h < ow ? kw + h : kw) * 8) * kTabPitch, wv[h]);
+              pown += kw + h < ow ? x : 0.f;
+            }
           }
         }
         const bool skip_pub = fault_part == part && f == 0 && t == 0;  // fault injection (tests only)
@@ -3665,7 +3676,17 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
               }
             }
           }
-          for (int o = cw; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+          // xor reduction over the slices: distances 16 and 32 on the VALU (permlane swaps; the
+          // sum is commutative, so bitwise the shuffle's), shorter ones by ds_bpermute
+          for (int o = cw; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+          if (cw <= 16) {
+            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+            s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+          }
+          if (cw <= 32) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+            s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+          }
           if (sl == 0) {
             if (i < ncol) {
               const float sg = w[c] > 0.f ? 1.f : (w[c] < 0.f ? -1.f : 0.f);
