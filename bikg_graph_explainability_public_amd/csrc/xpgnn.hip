@@ -2714,6 +2714,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
 template <int FPL, bool GCN>
 __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
   constexpr int RIF = 8;
+  constexpr int RC = FPL >= 4 ? 4 : RIF;  // rows prefetched across targets (register budget)
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
   const uint32_t valid = a.nr >= 32 ? 0xFFFFFFFFu : ((1u << a.nr) - 1u);
@@ -2732,32 +2733,44 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
   int a_tf0 = 0, a_b0 = 0, a_b1 = 0;         // A state (lane copies of uniform values)
   int b_tf0 = 0, b_b0 = 0, b_b1 = 0, b_u0v = 0;  // B state
   uint32_t b_mv = 0u;
-  float b_self[FPL];
+  int b_sm = 0;
+  float b_self[FPL], b_root[FPL];  // own row of term 0 and of the ROOT term 1 (n_terms == 2)
   uint32_t c_kmv = 0u;                       // C state
-  float c_row[RIF][FPL];
+  float c_row[RC][FPL];
 #pragma unroll
-  for (int q = 0; q < FPL; ++q) b_self[q] = 0.f;
+  for (int q = 0; q < FPL; ++q) b_self[q] = b_root[q] = 0.f;
+  const float* T1 = a.table[a.n_terms > 1 ? 1 : 0] + lane * FPL;
+  float bv[FPL];  // loop-invariant (loaded once, not after every target's stores)
+#pragma unroll
+  for (int q = 0; q < FPL; ++q) bv[q] = lane * FPL + q < a.f_real ? a.bias[lane * FPL + q] : 0.f;
+  int64_t a_t = 0;
   auto issueA = [&](int64_t tn) {
+    a_t = tn;
     a_tf0 = a.tgt_f0[tn];
     a_b0 = pp[tn];
     a_b1 = pp[tn + 1];
   };
   auto issueB = [&]() {  // from A
+    const int64_t tn_b = a_t;
     b_tf0 = a_tf0;
     b_b0 = a_b0;
     b_b1 = a_b1;
     const int e = b_b0 + lane;
     b_u0v = e < b_b1 ? a.agg_f0[e] : 0;
     b_mv = a.mT0[b_tf0];
+    if (!GCN) b_sm = a.self_mult[(int64_t)r * a.n_tgt + tn_b];
 #pragma unroll
-    for (int q = 0; q < FPL; ++q) b_self[q] = T[(int64_t)b_tf0 * a.w_row + q];
+    for (int q = 0; q < FPL; ++q) {
+      b_self[q] = T[(int64_t)b_tf0 * a.w_row + q];
+      b_root[q] = a.n_terms == 2 ? T1[(int64_t)b_tf0 * a.w_row + q] : 0.f;
+    }
   };
   auto issueC = [&]() {  // from B
     const int e = b_b0 + lane;
     c_kmv = e < b_b1 ? a.mT0[b_u0v] : 0u;
-    const int ne = min(min(64, b_b1 - b_b0), RIF);
+    const int ne = min(min(64, b_b1 - b_b0), RC);
 #pragma unroll
-    for (int jj = 0; jj < RIF; ++jj) {
+    for (int jj = 0; jj < RC; ++jj) {
       const int u0 = __builtin_amdgcn_readlane(b_u0v, jj < ne ? jj : 0);
 #pragma unroll
       for (int q = 0; q < FPL; ++q) c_row[jj][q] = T[(int64_t)u0 * a.w_row + q];
@@ -2775,14 +2788,18 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
     const int b0 = __builtin_amdgcn_readfirstlane(b_b0), b1 = __builtin_amdgcn_readfirstlane(b_b1);
     const int u0v_first = b_u0v;
     const uint32_t kmv_first = c_kmv & mv;
-    float row0[RIF][FPL];
+    float row0[RC][FPL];
 #pragma unroll
-    for (int jj = 0; jj < RIF; ++jj)
+    for (int jj = 0; jj < RC; ++jj)
 #pragma unroll
       for (int q = 0; q < FPL; ++q) row0[jj][q] = c_row[jj][q];
-    float self[FPL];
+    float self[FPL], root[FPL];
 #pragma unroll
-    for (int q = 0; q < FPL; ++q) self[q] = b_self[q];
+    for (int q = 0; q < FPL; ++q) {
+      self[q] = b_self[q];
+      root[q] = b_root[q];
+    }
+    const int sm = GCN ? 0 : __builtin_amdgcn_readfirstlane(b_sm);
     const bool more = t + nw < a.n_tgt;
     if (more) issueB();                          // target t + nw (A issued one iteration ago)
     if (t + 2 * nw < a.n_tgt) issueA(t + 2 * nw);
@@ -2809,9 +2826,9 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
           const int j = j0 + jj < ne ? j0 + jj : j0;
           km[jj] = j0 + jj < ne ? __builtin_amdgcn_readlane(kmv, j) : 0u;
           const int u0 = __builtin_amdgcn_readlane(u0v, j);
-          if (first && j0 == 0) {  // scalar: the rows prefetched before the previous stores
+          if (first && j0 == 0 && jj < RC) {  // scalar: the rows prefetched before the previous stores
 #pragma unroll
-            for (int q = 0; q < FPL; ++q) row[jj][q] = row0[jj][q];
+            for (int q = 0; q < FPL; ++q) row[jj][q] = row0[jj < RC ? jj : 0][q];
           } else {
 #pragma unroll
             for (int q = 0; q < FPL; ++q) row[jj][q] = T[(int64_t)u0 * a.w_row + q];
@@ -2842,7 +2859,6 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
         }
       }
     }
-    const int sm = GCN ? 0 : __builtin_amdgcn_readfirstlane(a.self_mult[(int64_t)r * a.n_tgt + t]);
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
       if (GCN) {
@@ -2856,27 +2872,34 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
         for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(static_cast<float>(sm), self[q], tot[s][q]) * inv;
       }
     }
-    for (int k = 1; k < a.n_terms; ++k) {  // ROOT terms (host-checked)
-      const float* Tk = a.table[k] + lane * FPL;
+    for (int k = 1; k < a.n_terms; ++k) {  // ROOT terms (host-checked); term 1 prefetched
       float sk[FPL];
+      if (k == 1 && a.n_terms == 2) {
 #pragma unroll
-      for (int q = 0; q < FPL; ++q) sk[q] = Tk[(int64_t)tf0 * a.w_row + q];
+        for (int q = 0; q < FPL; ++q) sk[q] = root[q];
+      } else {
+        const float* Tk = a.table[k] + lane * FPL;
+#pragma unroll
+        for (int q = 0; q < FPL; ++q) sk[q] = Tk[(int64_t)tf0 * a.w_row + q];
+      }
 #pragma unroll
       for (int s = 0; s < 32; ++s)
 #pragma unroll
         for (int q = 0; q < FPL; ++q) tot[s][q] += sk[q];
     }
-    float bv[FPL];
-#pragma unroll
-    for (int q = 0; q < FPL; ++q) bv[q] = lane * FPL + q < a.f_real ? a.bias[lane * FPL + q] : 0.f;
     if (more) issueC();  // before the stores (see above)
     float* o = a.out + (int64_t)t * 32 * a.w_row + lane * FPL;
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
       if (s < a.nr) {
         float v[FPL];
+        if (a.act == XPG_ACT_RELU) {  // one scalar branch, not a runtime switch per value
 #pragma unroll
-        for (int q = 0; q < FPL; ++q) v[q] = lane * FPL + q < a.f_real ? act_apply(tot[s][q] + bv[q], a.act) : 0.f;
+          for (int q = 0; q < FPL; ++q) v[q] = lane * FPL + q < a.f_real ? fmaxf(tot[s][q] + bv[q], 0.f) : 0.f;
+        } else {
+#pragma unroll
+          for (int q = 0; q < FPL; ++q) v[q] = lane * FPL + q < a.f_real ? act_apply(tot[s][q] + bv[q], a.act) : 0.f;
+        }
         if (FPL == 2) {
           *reinterpret_cast<float2*>(o + s * a.w_row) = make_float2(v[0], v[1]);
         } else {
