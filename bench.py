@@ -219,6 +219,8 @@ def headline(args, dev, world, rank):
     f0, f1 = sharding.shard_range(times, world, rank)
     params = {"lr": 0.01, "l1_lambda": 1e-4}
     stream = torch.cuda.current_stream()
+    side = torch.cuda.Stream(device=dev)
+    use_side = os.environ.get("XPG_SIDE_STREAM") != "0"  # sharding.gather_map_beside's switch
     w0 = torch.zeros((times, S), device=dev)
     statuses = []
     phases = ("sample", "forward", "shap", "gather", "wlm")
@@ -231,9 +233,15 @@ def headline(args, dev, world, rank):
         mk(0)
         bits = engine.sample_shapley(seed, r1 - r0, S, dev, row_offset=r0)
         mk(1)
+        # KernelSHAP on a side stream beside the forward (as Explainer.run does,
+        # sharding.gather_map_beside); "shap" = the wait for it after the forward
+        side.wait_stream(stream)
         y_loc = plan.forward(bits)[:, 0]
+        with torch.cuda.stream(side if use_side else stream):
+            k_loc = engine.shap_kernel(bits, S)
         mk(2)
-        k_loc = engine.shap_kernel(bits, S)
+        stream.wait_stream(side)
+        k_loc.record_stream(stream)
         mk(3)
         y = sharding.gather_rows(y_loc, n_rows)           # RCCL all-gather of the logits
         k = sharding.gather_rows(k_loc, n_rows)

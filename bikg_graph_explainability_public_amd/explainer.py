@@ -274,9 +274,19 @@ class Explainer:
         # its extraction re-cuts the [B] outputs (quirk Q4); params["hetero_q4"] = False keeps
         # the per-copy outputs instead (model.py:118-253, wlm.py:435-436)
         q4 = bool(self.params.get("hetero_q4", True))
+
+        def kernel_rows(s, e):
+            if e == s:
+                return torch.empty(0, dtype=torch.float64, device=device)
+            return engine.shap_kernel(flat[s:e], S)
+        kern = None
         if plan is not None:
-            y = sharding.gather_map(times * R, lambda s, e: plan.forward(flat[s:e])[:, 0],
-                                    g).reshape(times, R)
+            # KernelSHAP needs only the mask bits: its kernels run on a side stream beside the
+            # masked forward (sharding.gather_map_beside)
+            y, kern = sharding.gather_map_beside(times * R, lambda s, e: plan.forward(flat[s:e])[:, 0],
+                                                 kernel_rows, g)
+            y = y.reshape(times, R)
+            kern = kern.reshape(times, R)
             if getattr(plan, "multi_type", False):
                 empty = pipeline.empty_copy_rows(flat, S, sub_ei).reshape(times, R)
                 y = torch.stack([pipeline.multi_type_targets(y[i], empty[i], batch, sub_ind, S, q4)
@@ -298,11 +308,8 @@ class Explainer:
                 return torch.stack(ys) if ys else torch.empty((0, R), device=device)
             y = sharding.gather_map(times, generic, g)
 
-        def kernel_rows(s, e):
-            if e == s:
-                return torch.empty(0, dtype=torch.float64, device=device)
-            return engine.shap_kernel(flat[s:e], S)
-        kern = sharding.gather_map(times * R, kernel_rows, g).reshape(times, R)
+        if kern is None:
+            kern = sharding.gather_map(times * R, kernel_rows, g).reshape(times, R)
 
         fits = {}
 

@@ -14,6 +14,8 @@ Every rank ends with the same full tensors, so `weight_stacking` (mean / populat
 repeats) and the DataFrames are identical on every rank and identical to a single-GPU run.
 torch.distributed's all_gather needs equal shard shapes: shards are padded to the largest one.
 """
+import os
+
 import torch
 
 
@@ -124,3 +126,26 @@ def gather_map(n, fn, group=None):
     world, rank = world_info(group)
     s, e = shard_range(n, world, rank)
     return gather_rows(fn(s, e), n, group)
+
+
+def gather_map_beside(n, fn, side_fn, group=None):
+    """`gather_map(n, fn)` with a second row-sharded job run beside it on a side stream.
+
+    `side_fn(start, stop)` (e.g. the KernelSHAP weights of the shard, which need only the mask
+    bits) is launched right after `fn` (the masked forward) on its own HIP stream, so its small
+    kernels fill the CUs the forward leaves free instead of queueing behind it; both outputs
+    are then all-gathered.  Returns (gathered fn output, gathered side_fn output).  CPU
+    tensors / no GPU: sequential."""
+    world, rank = world_info(group)
+    s, e = shard_range(n, world, rank)
+    if not torch.cuda.is_available() or os.environ.get("XPG_SIDE_STREAM") == "0":
+        return gather_rows(fn(s, e), n, group), gather_rows(side_fn(s, e), n, group)
+    cur = torch.cuda.current_stream()
+    side = torch.cuda.Stream(device=cur.device)
+    side.wait_stream(cur)  # the inputs (mask bits) are produced on the current stream
+    main = fn(s, e)
+    with torch.cuda.stream(side):
+        other = side_fn(s, e)
+    cur.wait_stream(side)
+    other.record_stream(cur)  # allocated on the side stream, consumed on this one
+    return gather_rows(main, n, group), gather_rows(other, n, group)
