@@ -380,7 +380,7 @@ def full_graph_alg_bytes(n, e_kept_per_row, e, f_in, f_out, rows, layers=2):
     return layers * per_layer, per_layer
 
 
-C3_KERNELS = ("k_wide_bits", "k_wide_f0", "k_wide_degree", "k_wide_tgt")
+C3_KERNELS = ("k_wide_bits", "k_wide_f0", "k_wide_degree", "k_wide_l1s", "k_wide_last_ws")
 
 
 def c3_section(args, dev, world, rank):
