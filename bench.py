@@ -63,6 +63,9 @@ def parse():
     p.add_argument("--sections", default="all",
                    help="comma list of " + ",".join(SECTIONS) + " (PMC passes run one each)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-graph", action="store_true",
+                   help="headline at world 1: eager launches instead of replaying one captured "
+                        "HIP graph per step")
     p.add_argument("--cpu-rows", type=int, default=12800)
     p.add_argument("--cpu-procs", type=int, default=0,
                    help="CPU baseline worker processes (0: min(16, host cores))")
@@ -225,23 +228,37 @@ def headline(args, dev, world, rank):
     statuses = []
     phases = ("sample", "forward", "shap", "gather", "wlm")
     ev = {k: [] for k in phases}
+    # one process, one GPU: the step is replayed from ONE captured HIP graph (the path is
+    # host-launch-bound in eager mode: ~55 us of GPU idle per 0.3 ms step in the kernel trace);
+    # the sampler reads its seed from device memory and the graph advances it, so every replay
+    # draws new mask rows.  Multi-rank runs stay eager (the RCCL all-gathers are not captured).
+    use_graph = world == 1 and not args.no_graph
+    seed_t = torch.full((1,), 1000 + args.warmup, dtype=torch.int64, device=dev)
+    k_buf = torch.empty(r1 - r0, dtype=torch.float64, device=dev)
+    cnt_buf = torch.empty(r1 - r0, dtype=torch.int32, device=dev)
 
-    def step(i, record):
+    def step(i, record, dev_seed=False):
         marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
         mk = (lambda j: marks[j].record(stream)) if record else (lambda j: None)
         seed = 1000 + i
         mk(0)
-        bits = engine.sample_shapley(seed, r1 - r0, S, dev, row_offset=r0)
+        if dev_seed:
+            bits = engine.sample_shapley_dev(seed_t, r1 - r0, S, row_offset=r0)
+        else:
+            bits = engine.sample_shapley(seed, r1 - r0, S, dev, row_offset=r0)
         mk(1)
         # KernelSHAP on a side stream beside the forward (as Explainer.run does,
         # sharding.gather_map_beside); "shap" = the wait for it after the forward
         side.wait_stream(stream)
         y_loc = plan.forward(bits)[:, 0]
         with torch.cuda.stream(side if use_side else stream):
-            k_loc = engine.shap_kernel(bits, S)
+            # (graph capture: the side stream must not allocate; its buffers are static)
+            k_loc = engine.shap_kernel(bits, S, out=k_buf, scratch=cnt_buf) if dev_seed else \
+                engine.shap_kernel(bits, S)
         mk(2)
         stream.wait_stream(side)
-        k_loc.record_stream(stream)
+        if not dev_seed:  # (a captured graph's memory is private until the graph is freed)
+            k_loc.record_stream(stream)
         mk(3)
         y = sharding.gather_rows(y_loc, n_rows)           # RCCL all-gather of the logits
         k = sharding.gather_rows(k_loc, n_rows)
@@ -261,14 +278,32 @@ def headline(args, dev, world, rank):
             for j, name in enumerate(phases):
                 ev[name].append((marks[j], marks[j + 1]))
         w_all = sharding.gather_rows(w.reshape(f1 - f0, S), times)
-        return w_all.mean(0), w_all.std(0, unbiased=False)
+        out = (w_all.mean(0), w_all.std(0, unbiased=False))
+        if dev_seed:
+            seed_t.add_(1)  # the next replay's masks
+        return out
 
     for i in range(args.warmup):
         step(i, False)
+    if use_graph:
+        # the phase breakdown comes from 3 eager steps outside the timed region (events cannot
+        # split a graph replay); then one eager dev-seed step and the capture
+        for i in range(3):
+            step(args.warmup + i, True)
+        step(0, False, dev_seed=True)
+        seed_t.fill_(1000 + args.warmup)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step(0, False, dev_seed=True)
+        torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, True)
+        if use_graph:
+            graph.replay()
+        else:
+            step(args.warmup + i, True)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
@@ -300,7 +335,10 @@ def headline(args, dev, world, rank):
                    "parallelism": f"dp{world}: rows of the step's {times} repeat(s) sharded over "
                                   "ranks, RCCL all-gather of logits + kernel weights, fits "
                                   "sharded by repeat",
-                   "mask_sampler": "device (Philox Shapley)"},
+                   "mask_sampler": "device (Philox Shapley)",
+                   "launch": ("one captured HIP graph replayed per step (device-resident sampler "
+                              "seed advanced inside the graph); phases_ms from eager steps"
+                              if use_graph else "eager")},
         "phases_ms": phase_ms,
         "roofline": dict(roofline(wl, phase_ms["wlm"] * 1e-3, "headline", WLM_KERNELS),
                          kernel="surrogate fit chain (" + ", ".join(WLM_KERNELS) + ")",

@@ -136,8 +136,9 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
 template <int ALIGN>
 __global__ __launch_bounds__(256) void k_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
                                                  int words, uint32_t* __restrict__ bits,
-                                                 int32_t* __restrict__ counts) {
+                                                 int32_t* __restrict__ counts, const uint64_t* __restrict__ seed_dev) {
   __shared__ int red[4];
+  if (seed_dev) seed = *seed_dev;  // device-resident seed (graph replays draw new rows)
   const int quads = (words + 3) / 4;
   const int q = blockIdx.x * 256 + threadIdx.x;
   const int tail = static_cast<int>(cols & 31);
@@ -3028,8 +3029,12 @@ __global__ __launch_bounds__(256) void k_wlm_prep(const float* __restrict__ y, c
                                                   int words, int batch, int bw, int64_t steps, xpg_wlm_params P,
                                                   int64_t step0, WlmStep* __restrict__ st,
                                                   uint32_t* __restrict__ colbits, uint64_t* __restrict__ clr,
-                                                  int64_t n_clr, uint32_t* __restrict__ clr32, int n_clr32) {
+                                                  int64_t n_clr, uint32_t* __restrict__ clr32, int n_clr32,
+                                                  uint32_t* __restrict__ ep) {
   const int64_t fit = blockIdx.y;
+  // the exchange tags' device epoch advances once per fit chain (a replayed HIP graph carries
+  // the host epoch of its capture; this word makes every replay's tags new)
+  if (ep && blockIdx.x == 0 && fit == 0 && threadIdx.x == 0) *ep = *ep + 1u;
   if ((int64_t)blockIdx.x < steps) {
     wlm_stats_block(y, kern, rows, batch, P, step0, st, clr, n_clr, clr32, n_clr32, blockIdx.x, fit, steps,
                     steps * gridDim.y, fit * steps + blockIdx.x);
@@ -3429,7 +3434,12 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     const double* __restrict__ kern,
     const WlmStep* __restrict__ stp, xpg_wlm_params Pm, float* __restrict__ wg, float* __restrict__ mg,
     float* __restrict__ vg, float* __restrict__ p_hist, float* __restrict__ w_hist, uint64_t* xp,
-    uint32_t* err, uint32_t spin_limit, int fault_part, uint32_t epoch, int plain_ok) {
+    uint32_t* err, uint32_t spin_limit, int fault_part, uint32_t epoch_host, int plain_ok,
+    const uint32_t* __restrict__ ep_dev) {
+  // granule tag epoch (16 bits, never 0): the host's per-call counter + the device word that
+  // k_wlm_prep advances per chain, so replays of a captured launch get fresh tags too
+  uint32_t epoch = (epoch_host + (ep_dev ? *ep_dev : 0u)) & 0xFFFFu;
+  if (epoch == 0u) epoch = 1u;
   static_assert(sizeof(WlmStep) == 48, "WlmStep is read as 12 dwords");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int abort_s;  // set by any lane whose poll timed out (or saw the error word): leave the step loop
@@ -4712,18 +4722,18 @@ int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t ro
 }
 
 int launch_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits, int32_t* counts,
-                   hipStream_t st) {
+                   hipStream_t st, const uint64_t* seed_dev = nullptr) {
   const int words = words_of(cols);
   const int quads = (words + 3) / 4;
   if (rows == 0) return XPG_OK;
   XPG_REQ(quads <= (1 << 30), "shapley: row too long");
   const dim3 grid(static_cast<unsigned>(cdiv(quads, 256)), static_cast<unsigned>(std::min<int64_t>(rows, 65535)));
   if (words % 4 == 0)
-    hipLaunchKernelGGL(k_shapley<4>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts);
+    hipLaunchKernelGGL(k_shapley<4>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts, seed_dev);
   else if (words % 2 == 0)
-    hipLaunchKernelGGL(k_shapley<2>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts);
+    hipLaunchKernelGGL(k_shapley<2>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts, seed_dev);
   else
-    hipLaunchKernelGGL(k_shapley<1>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts);
+    hipLaunchKernelGGL(k_shapley<1>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts, seed_dev);
   XPG_LAUNCHED();
   return XPG_OK;
 }
@@ -4766,6 +4776,12 @@ int xpg_unpack_masks(const uint32_t* bits, int64_t rows, int64_t cols, uint8_t* 
 int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits, xpg_stream_t stream) {
   XPG_REQ(rows >= 0 && cols > 0 && row_offset >= 0, "shapley: bad shape");
   return launch_shapley(seed, row_offset, rows, cols, bits, nullptr, S(stream));
+}
+
+int xpg_sample_shapley_dev(const uint64_t* seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits,
+                           xpg_stream_t stream) {
+  XPG_REQ(seed && rows >= 0 && cols > 0 && row_offset >= 0, "shapley: bad shape");
+  return launch_shapley(0, row_offset, rows, cols, bits, nullptr, S(stream), seed);
 }
 
 int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits,
@@ -5000,7 +5016,7 @@ struct WlmWs {
   // multi-workgroup fit
   bool mc, xcd;
   int P, wpp, mc_ds, mc_cpl, mc_stg;
-  size_t xp_off, cnt_off, lds_mc;
+  size_t xp_off, cnt_off, ep_off, lds_mc;
   // grid (many-column) fit
   bool grid;
   int n_wg, n_tk;
@@ -5149,6 +5165,8 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   off += align_up(L->mc ? F * sizeof(uint64_t) * (2 * L->P * (size_t)batch + L->P) : 0);
   L->cnt_off = off;  // [F] (unused) + error word + [F] loss arrival counters
   off += align_up(sizeof(uint32_t) * (2 * F + 1));
+  L->ep_off = off;   // device epoch word (not cleared)
+  off += align_up(sizeof(uint32_t));
   L->total = off;
   return XPG_OK;
 }
@@ -5230,7 +5248,8 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   hipLaunchKernelGGL(k_wlm_prep, dim3(static_cast<unsigned>(steps + cdiv(lanes, 256)), nf), dim3(256), 0, st, y,
                      kernel, bits, rows, ic, words, ib, L.bw, steps, *params, step0, stp, colbits,
                      L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
-                     reinterpret_cast<uint32_t*>(ws + L.cnt_off), static_cast<int>(2 * n_fits + 1));
+                     reinterpret_cast<uint32_t*>(ws + L.cnt_off), static_cast<int>(2 * n_fits + 1),
+                     reinterpret_cast<uint32_t*>(ws + L.ep_off));
   XPG_LAUNCHED();
   bool launched = false;
   const uint32_t* errw = nullptr;
@@ -5255,7 +5274,8 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
                                   hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_mc))); \
       hipLaunchKernelGGL((k_wlm_fit_mc<C, G>), grid, dim3(1024), L.lds_mc, st, bits, colbits, rows, ic, words, ib, \
                          L.bw, L.P, L.wpp, L.mc_ds, n_fits, L.xcd ? 1 : 0, kernel, stp, *params, w, adam_m,      \
-                         adam_v, p_hist, w_hist, xp, cnt + n_fits, spin, fault, epoch, plain_ok);            \
+                         adam_v, p_hist, w_hist, xp, cnt + n_fits, spin, fault, epoch, plain_ok,             \
+                         reinterpret_cast<const uint32_t*>(ws + L.ep_off));                                  \
       XPG_LAUNCHED();                                                                                       \
       launched = true;                                                                                      \
     }

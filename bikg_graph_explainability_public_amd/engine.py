@@ -66,6 +66,19 @@ def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0,
     return bits, counts
 
 
+def sample_shapley_dev(seed: torch.Tensor, rows: int, cols: int, row_offset: int = 0):
+    """`sample_shapley` with the seed read on the device from `seed` (int64 [1], the bits of a
+    uint64) when the kernel runs: a captured HIP graph draws new rows on every replay once the
+    caller advances the tensor on the stream (xpg_sample_shapley_dev)."""
+    _lib.require_device(seed, "seed")
+    if seed.dtype != torch.int64 or seed.numel() != 1:
+        raise ValueError("seed must be a device int64 tensor of one element")
+    bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=seed.device)
+    call("xpg_sample_shapley_dev", ptr(seed), row_offset, rows, cols, ptr(bits),
+         _lib.stream_of(seed.device))
+    return bits
+
+
 def community_columns(communities, cols):
     """Column -> community CSR (int32 col_ptr [cols+1], col_comm [nnz]) of a community list."""
     lens = np.array([len(c) for c in communities], dtype=np.int64)
@@ -153,15 +166,25 @@ def khop_subgraph(node_idx: int, num_hops: int, edge_index: torch.Tensor, num_no
 
 
 # ----------------------------------------------------------------------------- KernelSHAP
-def shap_kernel(bits: torch.Tensor, cols: int, counts: torch.Tensor = None) -> torch.Tensor:
+def shap_kernel(bits: torch.Tensor, cols: int, counts: torch.Tensor = None,
+                out: torch.Tensor = None, scratch: torch.Tensor = None) -> torch.Tensor:
     """Kernel.compute (kernels.py:115-174) on device: fp64 [rows].  `counts` (row popcounts from
-    `sample_shapley(..., with_counts=True)`) skips the popcount pass over the bits."""
+    `sample_shapley(..., with_counts=True)`) skips the popcount pass over the bits.  `out`
+    (fp64 [rows]) and `scratch` (int32 [rows], the popcounts) let a caller that launches this on
+    a side stream inside a graph capture avoid allocating there."""
     _lib.require_device(bits, "bits")
     rows = bits.shape[0]
-    out = torch.empty(rows, dtype=torch.float64, device=bits.device)
+    if out is None:
+        out = torch.empty(rows, dtype=torch.float64, device=bits.device)
+    elif out.dtype != torch.float64 or out.numel() != rows or not out.is_contiguous():
+        raise ValueError("out must be a contiguous float64 [rows] tensor")
     st = _lib.stream_of(bits.device)
     if counts is None:
-        counts = torch.empty(rows, dtype=torch.int32, device=bits.device)
+        if scratch is None:
+            scratch = torch.empty(rows, dtype=torch.int32, device=bits.device)
+        elif scratch.dtype != torch.int32 or scratch.numel() != rows or not scratch.is_contiguous():
+            raise ValueError("scratch must be a contiguous int32 [rows] tensor")
+        counts = scratch
         call("xpg_popcount_rows", ptr(bits), rows, cols, ptr(counts), st)
     else:
         _lib.require_device(counts, "counts")

@@ -14,6 +14,7 @@
  *   xpg_pack_masks / xpg_unpack_masks  — bool mask batches handed between masks.py and
  *                                        wlm.py (DataLoader batches, masks.py:197-229)
  *   xpg_sample_shapley                 — Mask.shapley_mask           masks.py:231-260
+ *   xpg_sample_shapley_dev             — same, device-resident seed (graph replays)
  *   xpg_sample_communities             — Mask.get_internal_mask / get_external_indices +
  *                                        Pathways.mask_generator (masks.py:81-194,
  *                                        pathways.py:234-385)
@@ -41,7 +42,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 10
+#define XPG_ABI_VERSION 11
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -67,6 +68,11 @@ int xpg_unpack_masks(const uint32_t* bits, int64_t rows, int64_t cols, uint8_t* 
 /* Shapley masks, P(bit) = 1/2, counter-based Philox4x32-10 keyed by (seed, global row). */
 int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
                        uint32_t* bits, xpg_stream_t stream);
+/* Same rows with the seed read from device memory (*seed, uint64) when the kernel runs: a captured
+ * HIP graph of the hot path draws new masks on every replay once the caller advances *seed on
+ * the stream (v11). */
+int xpg_sample_shapley_dev(const uint64_t* seed, int64_t row_offset, int64_t rows, int64_t cols,
+                           uint32_t* bits, xpg_stream_t stream);
 /* Same bits, plus counts[r] = popcount of row r (the KernelSHAP coalition sizes, kernels.py:144),
  * accumulated while sampling so KernelSHAP needs no second pass over the bits. */
 int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,

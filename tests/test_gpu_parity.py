@@ -112,6 +112,30 @@ def test_shapley_sampler_properties():
     assert not torch.equal(a, c)
 
 
+def test_shapley_sampler_device_seed_and_graph_replay():
+    """xpg_sample_shapley_dev (seed read on the device) gives the host-seeded rows bit for bit,
+    and a captured HIP graph that advances the seed tensor draws seed s, s+1, ... on its
+    replays (the bench's graph-replayed headline step relies on both)."""
+    e = _eng()
+    R, S = 1000, 1193
+    seed_t = torch.full((1,), 41, dtype=torch.int64, device=DEV)
+    assert torch.equal(e.sample_shapley_dev(seed_t, R, S, row_offset=77),
+                       e.sample_shapley(41, R, S, DEV, row_offset=77))
+    big = torch.full((1,), -5, dtype=torch.int64, device=DEV)  # the uint64 bits 2^64 - 5
+    assert torch.equal(e.sample_shapley_dev(big, 64, S), e.sample_shapley(2 ** 64 - 5, 64, S, DEV))
+    out = torch.empty((R, (S + 31) // 32), dtype=torch.int32, device=DEV)
+    e.sample_shapley_dev(seed_t, R, S)  # warm-up outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out.copy_(e.sample_shapley_dev(seed_t, R, S))
+        seed_t.add_(1)
+    for s in (41, 42, 43):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, e.sample_shapley(s, R, S, DEV))
+
+
 def _community_case(S, lens, samples, seed=0):
     from bikg_graph_explainability_public_amd.masks import Mask
     rng = np.random.default_rng(seed)
