@@ -84,6 +84,8 @@ _SIGS = {
     "xpg_wlm_workspace": ([c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)], c_i32),
     "xpg_wlm_fit": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, ctypes.POINTER(WlmParams), c_i64,
                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
+    "xpg_wlm_fit_from": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, ctypes.POINTER(WlmParams), c_vp,
+                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
     "xpg_khop_workspace": ([c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)], c_i32),
     "xpg_khop_subgraph": ([c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                            ctypes.c_size_t, c_vp], c_i32),

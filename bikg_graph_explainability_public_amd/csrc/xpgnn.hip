@@ -3030,8 +3030,18 @@ __global__ __launch_bounds__(256) void k_wlm_prep(const float* __restrict__ y, c
                                                   int64_t step0, WlmStep* __restrict__ st,
                                                   uint32_t* __restrict__ colbits, uint64_t* __restrict__ clr,
                                                   int64_t n_clr, uint32_t* __restrict__ clr32, int n_clr32,
-                                                  uint32_t* __restrict__ ep) {
+                                                  uint32_t* __restrict__ ep, const float* __restrict__ w0,
+                                                  float* __restrict__ w, float* __restrict__ m,
+                                                  float* __restrict__ v, int64_t n_wmv) {
   const int64_t fit = blockIdx.y;
+  if (w0) {  // fresh fit from w0 (xpg_wlm_fit_from): w = w0, Adam moments 0 — no separate launches
+    const int64_t nb = (int64_t)gridDim.x * gridDim.y, b = fit * gridDim.x + blockIdx.x;
+    for (int64_t e = b * blockDim.x + threadIdx.x; e < n_wmv; e += nb * blockDim.x) {
+      w[e] = w0[e];
+      m[e] = 0.f;
+      v[e] = 0.f;
+    }
+  }
   // the exchange tags' device epoch advances once per fit chain (a replayed HIP graph carries
   // the host epoch of its capture; this word makes every replay's tags new)
   if (ep && blockIdx.x == 0 && fit == 0 && threadIdx.x == 0) *ep = *ep + 1u;
@@ -5217,10 +5227,34 @@ int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   return XPG_OK;
 }
 
+static int wlm_fit_impl(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                        const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
+                        const float* w0, float* w, float* adam_m, float* adam_v, double* losses,
+                        int32_t* best_epoch, int32_t* status, void* workspace, size_t workspace_bytes,
+                        xpg_stream_t stream);
+
 int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                 const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
                 float* w, float* adam_m, float* adam_v, double* losses, int32_t* best_epoch,
                 int32_t* status, void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
+  return wlm_fit_impl(n_fits, bits, rows, cols, batch, y, kernel, params, step0, nullptr, w, adam_m, adam_v,
+                      losses, best_epoch, status, workspace, workspace_bytes, stream);
+}
+
+int xpg_wlm_fit_from(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                     const float* y, const double* kernel, const xpg_wlm_params* params, const float* w0,
+                     float* w, float* adam_m, float* adam_v, double* losses, int32_t* best_epoch,
+                     int32_t* status, void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
+  XPG_REQ(w0 != nullptr, "wlm_fit_from: w0 required");
+  return wlm_fit_impl(n_fits, bits, rows, cols, batch, y, kernel, params, 0, w0, w, adam_m, adam_v, losses,
+                      best_epoch, status, workspace, workspace_bytes, stream);
+}
+
+static int wlm_fit_impl(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                        const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
+                        const float* w0, float* w, float* adam_m, float* adam_v, double* losses,
+                        int32_t* best_epoch, int32_t* status, void* workspace, size_t workspace_bytes,
+                        xpg_stream_t stream) {
   XPG_REQ(params != nullptr, "wlm_fit: params required");
   XPG_REQ(n_fits <= 65535, "wlm_fit: at most 65535 fits per launch");
   XPG_REQ(rows / std::max<int64_t>(batch, 1) < 65535, "wlm_fit: at most 65534 steps per fit");
@@ -5231,8 +5265,16 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
   hipStream_t st = S(stream);
   char* ws = static_cast<char*>(workspace);
   WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
-  if (L.grid) return wlm_fit_grid(n_fits, bits, rows, cols, batch, y, kernel, *params, step0, w, adam_m, adam_v,
-                                  losses, best_epoch, status, ws, L, st);
+  if (L.grid) {
+    if (w0) {  // the grid fit has no prologue kernel: stream-ordered copy / clears
+      const size_t nb = sizeof(float) * (size_t)n_fits * (size_t)cols;
+      XPG_HIP(hipMemcpyAsync(w, w0, nb, hipMemcpyDeviceToDevice, st));
+      XPG_HIP(hipMemsetAsync(adam_m, 0, nb, st));
+      XPG_HIP(hipMemsetAsync(adam_v, 0, nb, st));
+    }
+    return wlm_fit_grid(n_fits, bits, rows, cols, batch, y, kernel, *params, step0, w, adam_m, adam_v,
+                        losses, best_epoch, status, ws, L, st);
+  }
   uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
   float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
   float* w_hist = reinterpret_cast<float*>(ws + L.whist_off);
@@ -5249,7 +5291,7 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
                      kernel, bits, rows, ic, words, ib, L.bw, steps, *params, step0, stp, colbits,
                      L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
                      reinterpret_cast<uint32_t*>(ws + L.cnt_off), static_cast<int>(2 * n_fits + 1),
-                     reinterpret_cast<uint32_t*>(ws + L.ep_off));
+                     reinterpret_cast<uint32_t*>(ws + L.ep_off), w0, w, adam_m, adam_v, n_fits * cols);
   XPG_LAUNCHED();
   bool launched = false;
   const uint32_t* errw = nullptr;

@@ -527,11 +527,20 @@ def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0,
         raise ValueError("batch_size should be a positive integer value, but got "
                          f"batch_size={batch}")
     nsteps = math.ceil(rows / batch)
-    w = w0.detach().to(device=dev, dtype=torch.float32).reshape(F, cols).clone()
-    m = torch.zeros((F, cols), dtype=torch.float32, device=dev) if m0 is None else \
-        m0.reshape(F, cols).clone()
-    v = torch.zeros((F, cols), dtype=torch.float32, device=dev) if v0 is None else \
-        v0.reshape(F, cols).clone()
+    # a fresh fit (no Adam state handed in) starts from w0 inside the fit's prologue kernel
+    # (xpg_wlm_fit_from): no copy / fill launches on the latency-bound chain
+    fresh = m0 is None and v0 is None and int(step0) == 0
+    w0f = w0.detach().to(device=dev, dtype=torch.float32).reshape(F, cols).contiguous()
+    if fresh:
+        w = torch.empty((F, cols), dtype=torch.float32, device=dev)
+        m = torch.empty((F, cols), dtype=torch.float32, device=dev)
+        v = torch.empty((F, cols), dtype=torch.float32, device=dev)
+    else:
+        w = w0f.clone()
+        m = torch.zeros((F, cols), dtype=torch.float32, device=dev) if m0 is None else \
+            m0.reshape(F, cols).clone()
+        v = torch.zeros((F, cols), dtype=torch.float32, device=dev) if v0 is None else \
+            v0.reshape(F, cols).clone()
     losses = torch.empty((F, nsteps), dtype=torch.float64, device=dev)
     best = torch.empty(F, dtype=torch.int32, device=dev)
     p = WlmParams(lr=abs(float(params["lr"])), l1_lambda=float(params["l1_lambda"]), beta1=0.9,
@@ -544,9 +553,14 @@ def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0,
     ws = _workspace(dev, n.value)
     if status is None:
         status = torch.empty(1, dtype=torch.int32, device=dev)
-    call("xpg_wlm_fit", F, ptr(bb), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
-         int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(status), ptr(ws),
-         ws.numel(), _lib.stream_of(dev))
+    if fresh:
+        call("xpg_wlm_fit_from", F, ptr(bb), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
+             ptr(w0f), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(status), ptr(ws),
+             ws.numel(), _lib.stream_of(dev))
+    else:
+        call("xpg_wlm_fit", F, ptr(bb), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
+             int(step0), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(status), ptr(ws),
+             ws.numel(), _lib.stream_of(dev))
     if check:
         check_fit_status(status)
     if not batched:

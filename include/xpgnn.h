@@ -212,6 +212,14 @@ int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols
                 const xpg_wlm_params* params, int64_t step0, float* w, float* adam_m,
                 float* adam_v, double* losses, int32_t* best_epoch, int32_t* status,
                 void* workspace, size_t workspace_bytes, xpg_stream_t stream);
+/* Same fit started from initial weights w0 [n_fits][cols] with zero Adam moments (step0 = 0):
+ * w = w0, adam_m = adam_v = 0 are written by the fit's own prologue kernel, so a fresh fit
+ * needs no copy / fill launches of its own (v11). */
+int xpg_wlm_fit_from(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols,
+                     int64_t batch, const float* y, const double* kernel,
+                     const xpg_wlm_params* params, const float* w0, float* w, float* adam_m,
+                     float* adam_v, double* losses, int32_t* best_epoch, int32_t* status,
+                     void* workspace, size_t workspace_bytes, xpg_stream_t stream);
 
 /* ---------------------------------------------------------------- k-hop computational subgraph */
 /* Replaces Data.comp_graph's PyG k_hop_subgraph(seed, hops, edge_index, relabel_nodes=True,

@@ -475,6 +475,30 @@ def test_wlm_fit_batched_independent_fits(wlm_path, F, S, monkeypatch):
         assert int(best[f]) == rb
 
 
+@pytest.mark.parametrize("wlm_path", ["single", "mc", "grid"])
+def test_wlm_fit_continuation_equals_one_fit(wlm_path, monkeypatch):
+    """A fresh fit (xpg_wlm_fit_from: w = w0, zero moments written by the fit's prologue) over
+    rows [0, R) gives bitwise the weights of the fit split in two calls: xpg_wlm_fit_from over
+    the first half of the batches, then xpg_wlm_fit continuing from its (w, m, v) with
+    step0 = the steps taken (Adam bias corrections keyed by the global step)."""
+    monkeypatch.setenv("XPG_WLM", wlm_path)
+    e = _eng()
+    rng = np.random.default_rng(17)
+    R, S, B = 1200, 640, 24
+    m = rng.random((R, S)) < 0.5
+    y = torch.as_tensor(rng.random(R).astype(np.float32))
+    k = torch.as_tensor(oracle.shap_kernel(m))
+    w0 = torch.as_tensor(((rng.random(S) - 0.5) * 0.1).astype(np.float32))
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    bits = e.pack_masks(torch.as_tensor(m).to(DEV))
+    w_all, _, _, _, _ = e.wlm_fit(bits, S, B, y, k, w0, params)
+    h = R // 2  # 25 whole batches
+    w1, _, _, m1, v1 = e.wlm_fit(bits[:h], S, B, y[:h], k[:h], w0, params)
+    w2, _, _, _, _ = e.wlm_fit(bits[h:], S, B, y[h:], k[h:], w1, params, m0=m1, v0=v1,
+                               step0=h // B)
+    assert torch.equal(w2, w_all)
+
+
 # ------------------------------------------------------------------ end to end
 @pytest.mark.parametrize("name", CASES)
 def test_explainer_run_matches_reference_dataframes(name):
