@@ -278,7 +278,8 @@ def headline(args, dev, world, rank):
             for j, name in enumerate(phases):
                 ev[name].append((marks[j], marks[j + 1]))
         w_all = sharding.gather_rows(w.reshape(f1 - f0, S), times)
-        out = (w_all.mean(0), w_all.std(0, unbiased=False))
+        std, mean = torch.std_mean(w_all, 0, unbiased=False)  # Explainer.weight_stacking
+        out = (mean, std)
         if dev_seed:
             seed_t.add_(1)  # the next replay's masks
         return out

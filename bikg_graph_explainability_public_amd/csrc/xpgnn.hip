@@ -180,6 +180,51 @@ __global__ __launch_bounds__(256) void k_shapley(uint64_t seed, int64_t row_offs
   }
 }
 
+// Short rows (fewer than 64 quads of words, e.g. a 1,193-column subgraph: 10 quads): one lane
+// per (row, quad) over a flat index, so a 256-lane block covers many rows instead of leaving
+// 246 of its lanes idle on one row.  Same Philox counters (quad, global row) — bit-identical
+// rows; per-row popcounts by one atomic add per lane.
+template <int ALIGN>
+__global__ __launch_bounds__(256) void k_shapley_flat(uint64_t seed, int64_t row_offset, int64_t rows,
+                                                      int64_t cols, int words, uint32_t* __restrict__ bits,
+                                                      int32_t* __restrict__ counts,
+                                                      const uint64_t* __restrict__ seed_dev) {
+  if (seed_dev) seed = *seed_dev;
+  const int quads = (words + 3) / 4;
+  const int tail = static_cast<int>(cols & 31);
+  const int64_t n = rows * quads;
+  for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < n;
+       gid += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = gid / quads;
+    const int q = static_cast<int>(gid - r * quads);
+    const uint64_t gr = static_cast<uint64_t>(row_offset + r);
+    const uint4 o = philox4x32_10(make_uint4(static_cast<uint32_t>(q), static_cast<uint32_t>(gr),
+                                             static_cast<uint32_t>(gr >> 32), 0x58504721u),
+                                  static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+    uint32_t v[4] = {o.x, o.y, o.z, o.w};
+    const int w0 = q * 4;
+    int pc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (w0 + j >= words) v[j] = 0u;
+      else if (w0 + j == words - 1 && tail) v[j] &= (1u << tail) - 1u;
+      pc += __popc(v[j]);
+    }
+    uint32_t* dst = bits + r * words + w0;
+    if (ALIGN == 4 && w0 + 4 <= words) {
+      *reinterpret_cast<uint4*>(dst) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else if (ALIGN == 2 && w0 + 4 <= words) {
+      reinterpret_cast<uint2*>(dst)[0] = make_uint2(v[0], v[1]);
+      reinterpret_cast<uint2*>(dst)[1] = make_uint2(v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (w0 + j < words) dst[j] = v[j];
+    }
+    if (counts && pc) atomicAdd(counts + r, pc);
+  }
+}
+
 // ------------------------------------------------------------------ community-aware masks
 // Device restatement of the community sampler (masks.py:81-194 + pathways.py:234-385): the
 // host lays out one block per community in length-descending order, blocks[b] = {row_start,
@@ -4737,6 +4782,20 @@ int launch_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols
   const int quads = (words + 3) / 4;
   if (rows == 0) return XPG_OK;
   XPG_REQ(quads <= (1 << 30), "shapley: row too long");
+  if (quads < 64) {  // short rows: lanes over (row, quad)
+    const unsigned nb = static_cast<unsigned>(std::min<int64_t>(cdiv(rows * quads, 256), 65535 * 8));
+    if (words % 4 == 0)
+      hipLaunchKernelGGL(k_shapley_flat<4>, dim3(nb), dim3(256), 0, st, seed, row_offset, rows, cols, words, bits,
+                         counts, seed_dev);
+    else if (words % 2 == 0)
+      hipLaunchKernelGGL(k_shapley_flat<2>, dim3(nb), dim3(256), 0, st, seed, row_offset, rows, cols, words, bits,
+                         counts, seed_dev);
+    else
+      hipLaunchKernelGGL(k_shapley_flat<1>, dim3(nb), dim3(256), 0, st, seed, row_offset, rows, cols, words, bits,
+                         counts, seed_dev);
+    XPG_LAUNCHED();
+    return XPG_OK;
+  }
   const dim3 grid(static_cast<unsigned>(cdiv(quads, 256)), static_cast<unsigned>(std::min<int64_t>(rows, 65535)));
   if (words % 4 == 0)
     hipLaunchKernelGGL(k_shapley<4>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts, seed_dev);

@@ -120,9 +120,10 @@ class Explainer:
 
     @staticmethod
     def weight_stacking(weights):
-        """explainer.py:288-314 — mean and population std over repeats."""
+        """explainer.py:288-314 — mean and population std over repeats (one fused reduction)."""
         stack = torch.vstack(weights)
-        return torch.mean(stack, 0), torch.std(stack, 0, unbiased=False)
+        std, mean = torch.std_mean(stack, 0, unbiased=False)
+        return mean, std
 
     # ------------------------------------------------------------------------------ run
     def prepare(self, element, device):

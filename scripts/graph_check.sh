@@ -1,6 +1,6 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "shapley or wlm or fit or explainer or run or golden or c5 or queries or sharded or smoke" > gpurun_out/graph_tests.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "shapley or sampler or communit or wlm or fit or explainer or run or golden or c5 or queries or sharded or smoke or counts" > gpurun_out/graph_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/graph_tests.log
 [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
