@@ -228,19 +228,23 @@ def headline(args, dev, world, rank):
     statuses = []
     phases = ("sample", "forward", "shap", "gather", "wlm")
     ev = {k: [] for k in phases}
-    # one process, one GPU: the step is replayed from ONE captured HIP graph (the path is
-    # host-launch-bound in eager mode: ~55 us of GPU idle per 0.3 ms step in the kernel trace);
-    # the sampler reads its seed from device memory and the graph advances it, so every replay
-    # draws new mask rows.  Multi-rank runs stay eager (the RCCL all-gathers are not captured).
-    use_graph = world == 1 and not args.no_graph
+    # The step is host-launch-bound in eager mode (~55 us of GPU idle per 0.3 ms step in the
+    # kernel trace), so it is replayed from captured HIP graphs: the sampler reads its seed from
+    # device memory and the graph advances it, so every replay draws new mask rows.  One
+    # process: ONE graph per step.  Several ranks: the RCCL all-gathers stay eager between two
+    # graphs (A: masks -> forward + KernelSHAP; B: the surrogate fit), nothing collective is
+    # captured (XPG_BENCH_SPLIT_GRAPH=1 runs this split form on one GPU too).
+    use_graph = not args.no_graph
+    split = world > 1 or os.environ.get("XPG_BENCH_SPLIT_GRAPH") == "1"
     seed_t = torch.full((1,), 1000 + args.warmup, dtype=torch.int64, device=dev)
     k_buf = torch.empty(r1 - r0, dtype=torch.float64, device=dev)
+    stash = {}
     cnt_buf = torch.empty(r1 - r0, dtype=torch.int32, device=dev)
 
-    def step(i, record, dev_seed=False):
-        marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
-        mk = (lambda j: marks[j].record(stream)) if record else (lambda j: None)
-        seed = 1000 + i
+    def part_a(seed, dev_seed, mk=lambda j: None):
+        """masks -> forward (+ KernelSHAP on the side stream): this rank's rows"""
+        # the CURRENT stream: inside a capture that is the capture stream, not `stream`
+        cur = torch.cuda.current_stream()
         mk(0)
         if dev_seed:
             bits = engine.sample_shapley_dev(seed_t, r1 - r0, S, row_offset=r0)
@@ -249,23 +253,28 @@ def headline(args, dev, world, rank):
         mk(1)
         # KernelSHAP on a side stream beside the forward (as Explainer.run does,
         # sharding.gather_map_beside); "shap" = the wait for it after the forward
-        side.wait_stream(stream)
+        side.wait_stream(cur)
         y_loc = plan.forward(bits)[:, 0]
-        with torch.cuda.stream(side if use_side else stream):
+        with torch.cuda.stream(side if use_side else cur):
             # (graph capture: the side stream must not allocate; its buffers are static)
             k_loc = engine.shap_kernel(bits, S, out=k_buf, scratch=cnt_buf) if dev_seed else \
                 engine.shap_kernel(bits, S)
         mk(2)
-        stream.wait_stream(side)
+        cur.wait_stream(side)
         if not dev_seed:  # (a captured graph's memory is private until the graph is freed)
-            k_loc.record_stream(stream)
+            k_loc.record_stream(cur)
         mk(3)
-        y = sharding.gather_rows(y_loc, n_rows)           # RCCL all-gather of the logits
-        k = sharding.gather_rows(k_loc, n_rows)
-        mk(4)
+        if dev_seed:
+            stash.update(bits=bits, y=y_loc, k=k_loc)
+        return bits, y_loc, k_loc
+
+    def part_b(seed, dev_seed, bits, y, k):
+        """this rank's repeats' surrogate fits"""
         if (f0 * R, f1 * R) == (r0, r1):
             fbits = bits
-        else:  # this rank's repeats straddle other shards: regenerate their rows (Philox)
+        elif dev_seed:  # this rank's repeats straddle other shards: regenerate their rows
+            fbits = engine.sample_shapley_dev(seed_t, (f1 - f0) * R, S, row_offset=f0 * R)
+        else:
             fbits = engine.sample_shapley(seed, (f1 - f0) * R, S, dev, row_offset=f0 * R)
         st = torch.empty(1, dtype=torch.int32, device=dev)
         w, _, _, _, _ = engine.wlm_fit(fbits.view(f1 - f0, R, -1), S, batch,
@@ -273,13 +282,29 @@ def headline(args, dev, world, rank):
                                        k[f0 * R:f1 * R].view(f1 - f0, R), w0[f0:f1], params,
                                        check=False, status=st)
         statuses.append(st)
+        if dev_seed:
+            stash.update(w=w, st=st)
+        return w
+
+    def part_c(w):
+        w_all = sharding.gather_rows(w.reshape(f1 - f0, S), times)
+        std, mean = torch.std_mean(w_all, 0, unbiased=False)  # Explainer.weight_stacking
+        return mean, std
+
+    def step(i, record, dev_seed=False):
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
+        mk = (lambda j: marks[j].record(stream)) if record else (lambda j: None)
+        seed = 1000 + i
+        bits, y_loc, k_loc = part_a(seed, dev_seed, mk)
+        y = sharding.gather_rows(y_loc, n_rows)           # RCCL all-gather of the logits
+        k = sharding.gather_rows(k_loc, n_rows)
+        mk(4)
+        w = part_b(seed, dev_seed, bits, y, k)
         mk(5)
         if record:
             for j, name in enumerate(phases):
                 ev[name].append((marks[j], marks[j + 1]))
-        w_all = sharding.gather_rows(w.reshape(f1 - f0, S), times)
-        std, mean = torch.std_mean(w_all, 0, unbiased=False)  # Explainer.weight_stacking
-        out = (mean, std)
+        out = part_c(w)
         if dev_seed:
             seed_t.add_(1)  # the next replay's masks
         return out
@@ -294,20 +319,58 @@ def headline(args, dev, world, rank):
         step(0, False, dev_seed=True)
         seed_t.fill_(1000 + args.warmup)
         torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step(0, False, dev_seed=True)
+        if not split:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                g_out = step(0, False, dev_seed=True)
+        else:
+            y_s = torch.empty(n_rows, dtype=torch.float32, device=dev)
+            k_s = torch.empty(n_rows, dtype=torch.float64, device=dev)
+            graph_a, graph_b = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph_a):
+                g_bits, g_y, g_k = part_a(0, True)
+            with torch.cuda.graph(graph_b, pool=graph_a.pool()):
+                g_w = part_b(0, True, g_bits, y_s, k_s)
+                seed_t.add_(1)
+
+            def split_step():
+                graph_a.replay()
+                y_s.copy_(sharding.gather_rows(g_y, n_rows))  # eager RCCL all-gathers
+                k_s.copy_(sharding.gather_rows(g_k, n_rows))
+                graph_b.replay()
+                return part_c(g_w)
         torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if use_graph:
+        if use_graph and not split:
             graph.replay()
+        elif use_graph:
+            out = split_step()
         else:
             step(args.warmup + i, True)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
+    graph_check = None
+    if use_graph:  # outside the timed region: the last replay == an eager step on the same seed
+        last = out if split else g_out
+        ref = step(args.warmup + args.steps - 1, False)
+        graph_check = max(float((last[0] - ref[0]).abs().max()), float((last[1] - ref[1]).abs().max()))
+        if os.environ.get("XPG_BENCH_DEBUG"):
+            sd = 1000 + args.warmup + args.steps - 1
+            b_e = engine.sample_shapley(sd, r1 - r0, S, dev, row_offset=r0)
+            y_e = plan.forward(b_e)[:, 0]
+            k_e = engine.shap_kernel(b_e, S)
+            w_e = engine.wlm_fit(b_e.view(1, R, -1), S, batch, y_e.view(1, R), k_e.view(1, R), w0, params)[0]
+            for nm, e in (("bits", b_e), ("y", y_e), ("k", k_e), ("w", w_e)):
+                g = stash[nm]
+                log(rank, f"stage {nm}: max|diff| {float((g.double() - e.double()).abs().max()):.3e} "
+                          f"nan {int(torch.isnan(g.double()).sum())} shape {tuple(g.shape)} vs {tuple(e.shape)}")
+            log(rank, f"status {int(stash['st'].item())} seed_t {int(seed_t.item())}")
+            log(rank, f"graph check: nan last {int(torch.isnan(last[0]).sum())}/{int(torch.isnan(last[1]).sum())} "
+                      f"ref {int(torch.isnan(ref[0]).sum())}/{int(torch.isnan(ref[1]).sum())} "
+                      f"last[:4] {last[0][:4].tolist()} ref[:4] {ref[0][:4].tolist()}")
     for st in statuses:  # outside the timed region: every fit's exchange status must be clean
         engine.check_fit_status(st)
     phase_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
@@ -337,10 +400,14 @@ def headline(args, dev, world, rank):
                                   "ranks, RCCL all-gather of logits + kernel weights, fits "
                                   "sharded by repeat",
                    "mask_sampler": "device (Philox Shapley)",
-                   "launch": ("one captured HIP graph replayed per step (device-resident sampler "
-                              "seed advanced inside the graph); phases_ms from eager steps"
-                              if use_graph else "eager")},
+                   "launch": ("eager" if not use_graph else
+                              ("two captured HIP graphs per step (masks -> forward + KernelSHAP; "
+                               "surrogate fit) with eager RCCL all-gathers between them"
+                               if split else "one captured HIP graph replayed per step") +
+                              " (device-resident sampler seed advanced inside the graph); "
+                              "phases_ms from eager steps")},
         "phases_ms": phase_ms,
+        "graph_check_max_abs_diff": graph_check,
         "roofline": dict(roofline(wl, phase_ms["wlm"] * 1e-3, "headline", WLM_KERNELS),
                          kernel="surrogate fit chain (" + ", ".join(WLM_KERNELS) + ")",
                          note="latency-bound (51 sequential Adam steps, SURVEY.md §8d regime "

@@ -19,7 +19,7 @@ def main():
     dev = torch.device("cuda", 0)
     lib = _lib.load()
     args = bench.parse()
-    arch, sub_feat, sub_ei, q, plan = bench.build_workload(args, dev)
+    arch, sub_feat, sub_ei, q, plan = bench.build_c2(args, dev)
     S = plan.cols
     bits = engine.sample_shapley(7, 12800, S, dev)
     names = ["prologue", "degree", "sync", "L2 agg (h1)", "sync", "dense L2", "head+y"]
