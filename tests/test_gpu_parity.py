@@ -308,6 +308,52 @@ def test_masked_forward_vs_oracle_fp64(fwd_path):
         np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)
 
 
+def test_captured_repeat_equals_eager():
+    """One repeat (device-seeded masks -> masked forward, KernelSHAP on a side stream ->
+    fresh surrogate fit) captured in a HIP graph, as bench.py's headline replays it: every
+    replay gives bitwise the eager repeat on seed s, s+1, ...  The side stream must fork from
+    the CAPTURE stream, or its kernels run once at capture time and never replay."""
+    e = _eng()
+    exp, z, meta, ctx, plan = _plan_for(CASES[0])
+    S, R, B = plan.cols, 640, 64
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    w0 = torch.zeros((1, S), device=DEV)
+    seed_t = torch.full((1,), 300, dtype=torch.int64, device=DEV)
+    k_buf = torch.empty(R, dtype=torch.float64, device=DEV)
+    cnt_buf = torch.empty(R, dtype=torch.int32, device=DEV)
+    st = torch.zeros(1, dtype=torch.int32, device=DEV)
+    side = torch.cuda.Stream(device=DEV)
+
+    def repeat(dev_seed, seed=None):
+        cur = torch.cuda.current_stream()
+        bits = e.sample_shapley_dev(seed_t, R, S) if dev_seed else e.sample_shapley(seed, R, S, DEV)
+        side.wait_stream(cur)
+        y = plan.forward(bits)[:, 0]
+        with torch.cuda.stream(side):
+            k = e.shap_kernel(bits, S, out=k_buf, scratch=cnt_buf) if dev_seed else e.shap_kernel(bits, S)
+        cur.wait_stream(side)
+        w = e.wlm_fit(bits.view(1, R, -1), S, B, y.view(1, R), k.view(1, R), w0, params,
+                      check=False, status=st)[0]
+        if dev_seed:
+            seed_t.add_(1)
+        return w
+
+    repeat(True)  # workspaces allocated outside the capture
+    seed_t.fill_(300)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        w_g = repeat(True)
+    for s in (300, 301, 302):
+        g.replay()
+        torch.cuda.synchronize()
+        e.check_fit_status(st)
+        w_e = repeat(False, s)
+        torch.cuda.synchronize()
+        assert torch.isfinite(w_g).all()
+        assert torch.equal(w_g, w_e), s
+
+
 @pytest.mark.parametrize("kind,dims,fc", [("gcn", [16, 32], [32, 1]),
                                            ("sage", [16, 32], [32, 8, 1]),
                                            ("gcn", [16, 128, 64], [64, 1]),
