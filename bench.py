@@ -83,8 +83,14 @@ def setup_dist():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        # XPG_BENCH_BACKEND=gloo + XPG_BENCH_ONE_GPU=1: a rehearsal of the N-rank path with
+        # every rank on cuda:0 (one-GPU box); the driver's runs use RCCL, one GPU per rank
+        if os.environ.get("XPG_BENCH_ONE_GPU") == "1":
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("XPG_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)}
+                                            if backend == "nccl" else {}))
     else:
         torch.cuda.set_device(0)
     return world, rank, local
@@ -236,6 +242,11 @@ def headline(args, dev, world, rank):
     # captured (XPG_BENCH_SPLIT_GRAPH=1 runs this split form on one GPU too).
     use_graph = not args.no_graph
     split = world > 1 or os.environ.get("XPG_BENCH_SPLIT_GRAPH") == "1"
+    # the pipelined graphs need each rank's fits to read only its own rows ((f0, f1) repeats
+    # == rows [r0, r1), e.g. times = world): the fit must not regenerate rows from seed_t
+    pipe = use_graph and (f0 * R, f1 * R) == (r0, r1) and \
+        os.environ.get("XPG_BENCH_PIPE", "1") == "1"
+    split = split and not pipe
     seed_t = torch.full((1,), 1000 + args.warmup, dtype=torch.int64, device=dev)
     k_buf = torch.empty(r1 - r0, dtype=torch.float64, device=dev)
     stash = {}
@@ -319,7 +330,60 @@ def headline(args, dev, world, rank):
         step(0, False, dev_seed=True)
         seed_t.fill_(1000 + args.warmup)
         torch.cuda.synchronize()
-        if not split:
+        if pipe:
+            # two graphs, ping-pong over two static sets of (bits, y, k): graph i fits the repeat
+            # in set i (capture stream) while the NEXT repeat's masks -> forward + KernelSHAP
+            # fill set 1 - i on side streams (allocation-free).  The fit is latency-bound on a
+            # few workgroups, the forward fills the rest of the chip.  Prologue (untimed): the
+            # first repeat's set; the timed K replays do K fits + K productions.
+            # Several ranks: each graph holds the fit + this rank's rows of the next repeat; the
+            # RCCL all-gathers of the next repeat's logits / kernel weights and the weight
+            # stacking stay eager after the replay (nothing collective is captured).
+            W_, nl = (S + 31) // 32, r1 - r0
+            sets = []
+            for _ in range(2):
+                d = dict(bits=torch.empty((nl, W_), dtype=torch.int32, device=dev),
+                         y=torch.empty((nl, plan.n_out), dtype=torch.float32, device=dev),
+                         k=torch.empty(nl, dtype=torch.float64, device=dev),
+                         cnt=torch.empty(nl, dtype=torch.int32, device=dev))
+                d["yf"] = torch.empty(n_rows, dtype=torch.float32, device=dev) if world > 1 \
+                    else d["y"][:, 0]
+                d["kf"] = torch.empty(n_rows, dtype=torch.float64, device=dev) if world > 1 \
+                    else d["k"]
+                sets.append(d)
+            s1 = torch.cuda.Stream(device=dev)
+
+            def produce(d):  # (in order on its stream: it is off the fit's critical path)
+                engine.sample_shapley_dev(seed_t, nl, S, row_offset=r0, out=d["bits"])
+                seed_t.add_(1)
+                plan.forward(d["bits"], out=d["y"])
+                engine.shap_kernel(d["bits"], S, out=d["k"], scratch=d["cnt"])
+
+            def exchange(d):  # eager RCCL all-gathers of a produced set (several ranks)
+                if world > 1:
+                    d["yf"].copy_(sharding.gather_rows(d["y"][:, 0], n_rows))
+                    d["kf"].copy_(sharding.gather_rows(d["k"], n_rows))
+
+            def pipe_step(i):
+                cur = torch.cuda.current_stream()
+                s1.wait_stream(cur)
+                w = part_b(0, True, sets[i]["bits"], sets[i]["yf"], sets[i]["kf"])
+                out = part_c(w) if world == 1 else w
+                with torch.cuda.stream(s1):
+                    produce(sets[1 - i])
+                cur.wait_stream(s1)
+                return out
+
+            produce(sets[0])  # prologue: the first timed step's repeat
+            exchange(sets[0])
+            torch.cuda.synchronize()
+            pipe_graphs, pipe_outs = [], []
+            for i in range(2):
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph):
+                    pipe_outs.append(pipe_step(i))
+                pipe_graphs.append(gph)
+        elif not split:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 g_out = step(0, False, dev_seed=True)
@@ -343,7 +407,12 @@ def headline(args, dev, world, rank):
     barrier(world)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if use_graph and not split:
+        if pipe:
+            pipe_graphs[i & 1].replay()
+            if world > 1:
+                exchange(sets[1 - (i & 1)])
+                out = part_c(pipe_outs[i & 1])
+        elif use_graph and not split:
             graph.replay()
         elif use_graph:
             out = split_step()
@@ -354,7 +423,8 @@ def headline(args, dev, world, rank):
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     graph_check = None
     if use_graph:  # outside the timed region: the last replay == an eager step on the same seed
-        last = out if split else g_out
+        last = (pipe_outs[(args.steps - 1) & 1] if world == 1 else out) if pipe else \
+            out if split else g_out
         ref = step(args.warmup + args.steps - 1, False)
         graph_check = max(float((last[0] - ref[0]).abs().max()), float((last[1] - ref[1]).abs().max()))
         if os.environ.get("XPG_BENCH_DEBUG"):
@@ -403,7 +473,11 @@ def headline(args, dev, world, rank):
                    "launch": ("eager" if not use_graph else
                               ("two captured HIP graphs per step (masks -> forward + KernelSHAP; "
                                "surrogate fit) with eager RCCL all-gathers between them"
-                               if split else "one captured HIP graph replayed per step") +
+                               if split else
+                              "two captured HIP graphs replayed alternately: step i's surrogate "
+                              "fit runs beside step i+1's masks -> forward + KernelSHAP "
+                              "(double-buffered; prologue untimed, K fits + K productions timed)"
+                              if pipe else "one captured HIP graph replayed per step") +
                               " (device-resident sampler seed advanced inside the graph); "
                               "phases_ms from eager steps")},
         "phases_ms": phase_ms,

@@ -66,14 +66,22 @@ def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0,
     return bits, counts
 
 
-def sample_shapley_dev(seed: torch.Tensor, rows: int, cols: int, row_offset: int = 0):
+def sample_shapley_dev(seed: torch.Tensor, rows: int, cols: int, row_offset: int = 0,
+                       out: torch.Tensor = None):
     """`sample_shapley` with the seed read on the device from `seed` (int64 [1], the bits of a
     uint64) when the kernel runs: a captured HIP graph draws new rows on every replay once the
-    caller advances the tensor on the stream (xpg_sample_shapley_dev)."""
+    caller advances the tensor on the stream (xpg_sample_shapley_dev).  `out` (int32
+    [rows, words]): write the rows there (no allocation, e.g. on a side stream in a capture)."""
     _lib.require_device(seed, "seed")
     if seed.dtype != torch.int64 or seed.numel() != 1:
         raise ValueError("seed must be a device int64 tensor of one element")
-    bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=seed.device)
+    if out is None:
+        bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=seed.device)
+    elif out.dtype != torch.int32 or tuple(out.shape) != (rows, words_of(cols)) or \
+            not out.is_contiguous():
+        raise ValueError("out must be a contiguous int32 [rows, ceil(cols / 32)] tensor")
+    else:
+        bits = out
     call("xpg_sample_shapley_dev", ptr(seed), row_offset, rows, cols, ptr(bits),
          _lib.stream_of(seed.device))
     return bits
@@ -461,12 +469,19 @@ class ForwardPlan:
         _lib.check(_lib.load().xpg_forward_workspace(ctypes.byref(self.desc), rows, ctypes.byref(n)))
         return n.value
 
-    def forward(self, bits: torch.Tensor, max_ws_bytes=8 << 30) -> torch.Tensor:
+    def forward(self, bits: torch.Tensor, max_ws_bytes=8 << 30, out: torch.Tensor = None) -> torch.Tensor:
         """y [rows, n_out] fp32: model output at each target of the last conv layer, per mask
-        row (wlm.py:349-436 for one batch, all batches at once)."""
+        row (wlm.py:349-436 for one batch, all batches at once).  `out`: a contiguous fp32
+        [rows, n_out] tensor to write y into (no allocation once the workspace exists)."""
         _lib.require_device(bits, "bits")
         rows = bits.shape[0]
-        y = torch.empty((rows, self.n_out), dtype=torch.float32, device=self.device)
+        if out is None:
+            y = torch.empty((rows, self.n_out), dtype=torch.float32, device=self.device)
+        elif out.dtype != torch.float32 or tuple(out.shape) != (rows, self.n_out) or \
+                not out.is_contiguous():
+            raise ValueError("out must be a contiguous float32 [rows, n_out] tensor")
+        else:
+            y = out
         if rows == 0:
             return y
         w1, w2 = self.workspace_bytes(1), self.workspace_bytes(2)
