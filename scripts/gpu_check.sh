@@ -29,8 +29,8 @@ for step in "$@"; do
     pmc)   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline && \
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
-    pmc_*) # per-section PMC passes: pmc_<section> (headline: 1 warmup + 3 eager phase steps + 1 eager
-           # graph warm-up + 5 graph replays = 10 ops;
+    pmc_*) # per-section PMC passes: pmc_<section> (headline fits: 1 warmup + 3 eager phase steps + 1 eager
+           # dev-seed step + 5 pipelined graph replays + 1 eager graph-check step = 11 ops;
            # c3 / gp: 1 warm-up + 3 timed forwards / repeats = 4 ops)
            sec=${step#pmc_}
            cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
