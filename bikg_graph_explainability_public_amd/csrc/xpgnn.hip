@@ -5291,6 +5291,45 @@ static int wlm_fit_impl(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
                         const float* w0, float* w, float* adam_m, float* adam_v, double* losses,
                         int32_t* best_epoch, int32_t* status, void* workspace, size_t workspace_bytes,
                         xpg_stream_t stream);
+static int wlm_launch_prep(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                           const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
+                           const float* w0, float* w, float* adam_m, float* adam_v, char* ws, const WlmWs& L,
+                           hipStream_t st);
+static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                          const double* kernel, const xpg_wlm_params* params, float* w, float* adam_m, float* adam_v,
+                          double* losses, int32_t* best_epoch, int32_t* status, char* ws, const WlmWs& L,
+                          hipStream_t st);
+
+int xpg_wlm_prepare(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                    const float* y, const double* kernel, const xpg_wlm_params* params, const float* w0,
+                    float* w, float* adam_m, float* adam_v, void* workspace, size_t workspace_bytes,
+                    xpg_stream_t stream) {
+  XPG_REQ(params != nullptr && w0 != nullptr, "wlm_prepare: params and w0 required");
+  XPG_REQ(n_fits <= 65535, "wlm_fit: at most 65535 fits per launch");
+  XPG_REQ(rows / std::max<int64_t>(batch, 1) < 65535, "wlm_fit: at most 65534 steps per fit");
+  WlmWs L;
+  int rc = wlm_layout(n_fits, rows, cols, batch, &L);
+  if (rc) return rc;
+  XPG_REQ(workspace_bytes >= L.total, "wlm_fit: workspace too small");
+  XPG_REQ(!L.grid, "wlm_prepare: this shape takes the grid fit (no prologue kernel); use xpg_wlm_fit_from");
+  return wlm_launch_prep(n_fits, bits, rows, cols, batch, y, kernel, params, 0, w0, w, adam_m, adam_v,
+                         static_cast<char*>(workspace), L, S(stream));
+}
+
+int xpg_wlm_fit_prepared(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                         const double* kernel, const xpg_wlm_params* params, float* w, float* adam_m,
+                         float* adam_v, double* losses, int32_t* best_epoch, int32_t* status, void* workspace,
+                         size_t workspace_bytes, xpg_stream_t stream) {
+  XPG_REQ(params != nullptr, "wlm_fit: params required");
+  XPG_REQ(n_fits <= 65535, "wlm_fit: at most 65535 fits per launch");
+  WlmWs L;
+  int rc = wlm_layout(n_fits, rows, cols, batch, &L);
+  if (rc) return rc;
+  XPG_REQ(workspace_bytes >= L.total, "wlm_fit: workspace too small");
+  XPG_REQ(!L.grid, "wlm_fit_prepared: this shape takes the grid fit; use xpg_wlm_fit_from");
+  return wlm_launch_fit(n_fits, bits, rows, cols, batch, kernel, params, w, adam_m, adam_v, losses, best_epoch,
+                        status, static_cast<char*>(workspace), L, S(stream));
+}
 
 int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                 const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
@@ -5323,7 +5362,6 @@ static int wlm_fit_impl(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   XPG_REQ(workspace_bytes >= L.total, "wlm_fit: workspace too small");
   hipStream_t st = S(stream);
   char* ws = static_cast<char*>(workspace);
-  WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
   if (L.grid) {
     if (w0) {  // the grid fit has no prologue kernel: stream-ordered copy / clears
       const size_t nb = sizeof(float) * (size_t)n_fits * (size_t)cols;
@@ -5334,6 +5372,44 @@ static int wlm_fit_impl(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
     return wlm_fit_grid(n_fits, bits, rows, cols, batch, y, kernel, *params, step0, w, adam_m, adam_v,
                         losses, best_epoch, status, ws, L, st);
   }
+  int rc2 = wlm_launch_prep(n_fits, bits, rows, cols, batch, y, kernel, params, step0, w0, w, adam_m, adam_v, ws, L,
+                            st);
+  if (rc2) return rc2;
+  return wlm_launch_fit(n_fits, bits, rows, cols, batch, kernel, params, w, adam_m, adam_v, losses, best_epoch,
+                        status, ws, L, st);
+}
+
+// k_wlm_prep: the per-step constants (+ exchange slot clearing, epoch advance, optional fresh
+// start w = w0, m = v = 0) and the column bit vectors, one launch
+static int wlm_launch_prep(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                           const float* y, const double* kernel, const xpg_wlm_params* params, int64_t step0,
+                           const float* w0, float* w, float* adam_m, float* adam_v, char* ws, const WlmWs& L,
+                           hipStream_t st) {
+  WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
+  uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
+  const int64_t steps = cdiv(rows, batch);
+  const int words = words_of(cols);
+  const int ic = static_cast<int>(cols), ib = static_cast<int>(batch);
+  const unsigned nf = static_cast<unsigned>(n_fits);
+  // the multi-workgroup fit's exchange slots and error words are cleared by k_wlm_prep
+  const int64_t n_xp = L.mc ? n_fits * (2 * L.P * batch + L.P) : 0;
+  const int64_t lanes = steps * L.bw * words;
+  hipLaunchKernelGGL(k_wlm_prep, dim3(static_cast<unsigned>(steps + cdiv(lanes, 256)), nf), dim3(256), 0, st, y,
+                     kernel, bits, rows, ic, words, ib, L.bw, steps, *params, step0, stp, colbits,
+                     L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
+                     reinterpret_cast<uint32_t*>(ws + L.cnt_off), static_cast<int>(2 * n_fits + 1),
+                     reinterpret_cast<uint32_t*>(ws + L.ep_off), w0, w, adam_m, adam_v, n_fits * cols);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
+// the fit proper (multi-workgroup or one-workgroup kernel) + losses / best epoch / status, on a
+// workspace k_wlm_prep has prepared
+static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                          const double* kernel, const xpg_wlm_params* params, float* w, float* adam_m, float* adam_v,
+                          double* losses, int32_t* best_epoch, int32_t* status, char* ws, const WlmWs& L,
+                          hipStream_t st) {
+  WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
   uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
   float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
   float* w_hist = reinterpret_cast<float*>(ws + L.whist_off);
@@ -5342,16 +5418,6 @@ static int wlm_fit_impl(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   const int words = words_of(cols);
   const int ic = static_cast<int>(cols), ib = static_cast<int>(batch);
   const unsigned nf = static_cast<unsigned>(n_fits);
-  // the multi-workgroup fit's exchange slots and error words are cleared by k_wlm_prep
-  const int64_t n_xp = L.mc ? n_fits * (2 * L.P * batch + L.P) : 0;
-  // one launch: the per-step constants (+ exchange slot clearing) and the column bit vectors
-  const int64_t lanes = steps * L.bw * words;
-  hipLaunchKernelGGL(k_wlm_prep, dim3(static_cast<unsigned>(steps + cdiv(lanes, 256)), nf), dim3(256), 0, st, y,
-                     kernel, bits, rows, ic, words, ib, L.bw, steps, *params, step0, stp, colbits,
-                     L.mc ? reinterpret_cast<uint64_t*>(ws + L.xp_off) : nullptr, n_xp,
-                     reinterpret_cast<uint32_t*>(ws + L.cnt_off), static_cast<int>(2 * n_fits + 1),
-                     reinterpret_cast<uint32_t*>(ws + L.ep_off), w0, w, adam_m, adam_v, n_fits * cols);
-  XPG_LAUNCHED();
   bool launched = false;
   const uint32_t* errw = nullptr;
   if (L.mc) {

@@ -524,6 +524,52 @@ def check_fit_status(status):
             "XPG_WLM=single selects the single-workgroup fit.")
 
 
+class PreparedFit:
+    """A fresh surrogate fit (`wlm_fit` from w0) split in its two launches on static buffers of
+    one shape (xpg_wlm_prepare / xpg_wlm_fit_prepared, ABI v12): `prepare` runs the prologue
+    (per-step constants, column bit vectors, w = w0, zero Adam moments), `fit` the Adam steps and
+    returns w [F, cols].  Nothing is allocated after construction, so both can be captured on
+    any stream; with two instances the next fit is prepared while the current one runs.
+    `status` is the device status word (check_fit_status)."""
+
+    def __init__(self, n_fits, rows, cols, batch, params, device):
+        self.shape = (int(n_fits), int(rows), int(cols), int(batch))
+        n = ctypes.c_size_t(0)
+        _lib.check(_lib.load().xpg_wlm_workspace(n_fits, rows, cols, batch, ctypes.byref(n)))
+        self.ws = torch.empty(max(n.value, 1), dtype=torch.uint8, device=device)
+        self.w = torch.empty((n_fits, cols), dtype=torch.float32, device=device)
+        self.m = torch.empty_like(self.w)
+        self.v = torch.empty_like(self.w)
+        self.losses = torch.empty((n_fits, math.ceil(rows / batch)), dtype=torch.float64, device=device)
+        self.best = torch.empty(n_fits, dtype=torch.int32, device=device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=device)
+        self.p = WlmParams(lr=abs(float(params["lr"])), l1_lambda=float(params["l1_lambda"]), beta1=0.9,
+                           beta2=0.999, eps=1e-8, weight_decay=1e-2)
+
+    def _check(self, name, t, dtype, numel):
+        if t.dtype != dtype or t.numel() != numel or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {dtype} tensor of {numel} elements")
+
+    def prepare(self, bits, y, kernel, w0):
+        F, R, S, B = self.shape
+        self._check("bits", bits, torch.int32, F * R * words_of(S))
+        self._check("y", y, torch.float32, F * R)
+        self._check("kernel", kernel, torch.float64, F * R)
+        self._check("w0", w0, torch.float32, F * S)
+        call("xpg_wlm_prepare", F, ptr(bits), R, S, B, ptr(y), ptr(kernel), ctypes.byref(self.p),
+             ptr(w0), ptr(self.w), ptr(self.m), ptr(self.v), ptr(self.ws), self.ws.numel(),
+             _lib.stream_of(bits.device))
+
+    def fit(self, bits, kernel):
+        F, R, S, B = self.shape
+        self._check("bits", bits, torch.int32, F * R * words_of(S))
+        self._check("kernel", kernel, torch.float64, F * R)
+        call("xpg_wlm_fit_prepared", F, ptr(bits), R, S, B, ptr(kernel), ctypes.byref(self.p),
+             ptr(self.w), ptr(self.m), ptr(self.v), ptr(self.losses), ptr(self.best), ptr(self.status),
+             ptr(self.ws), self.ws.numel(), _lib.stream_of(bits.device))
+        return self.w
+
+
 def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0, check=True,
             status=None):
     """train_model (wlm.py:132-278) epoch loop on device for one or many independent fits.

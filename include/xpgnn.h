@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 11
+#define XPG_ABI_VERSION 12
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -220,6 +220,20 @@ int xpg_wlm_fit_from(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t
                      const xpg_wlm_params* params, const float* w0, float* w, float* adam_m,
                      float* adam_v, double* losses, int32_t* best_epoch, int32_t* status,
                      void* workspace, size_t workspace_bytes, xpg_stream_t stream);
+/* xpg_wlm_fit_from in two launches on one workspace (v12): xpg_wlm_prepare runs the fit's
+ * prologue (per-step constants from y / kernel, column bit vectors, w = w0, zero moments,
+ * exchange-slot reset) and xpg_wlm_fit_prepared the Adam steps + losses / best epoch / status.
+ * Same results bit for bit; a caller with two workspaces can prepare the next fit while the
+ * current one runs.  Shapes that take the many-column grid fit have no prologue: EINVAL. */
+int xpg_wlm_prepare(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols,
+                    int64_t batch, const float* y, const double* kernel,
+                    const xpg_wlm_params* params, const float* w0, float* w, float* adam_m,
+                    float* adam_v, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
+int xpg_wlm_fit_prepared(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols,
+                         int64_t batch, const double* kernel, const xpg_wlm_params* params,
+                         float* w, float* adam_m, float* adam_v, double* losses,
+                         int32_t* best_epoch, int32_t* status, void* workspace,
+                         size_t workspace_bytes, xpg_stream_t stream);
 
 /* ---------------------------------------------------------------- k-hop computational subgraph */
 /* Replaces Data.comp_graph's PyG k_hop_subgraph(seed, hops, edge_index, relabel_nodes=True,

@@ -308,6 +308,34 @@ def test_masked_forward_vs_oracle_fp64(fwd_path):
         np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("S, R, B", [(1193, 12800, 256), (300, 640, 64)])
+def test_prepared_fit_equals_fit_from(S, R, B):
+    """xpg_wlm_prepare + xpg_wlm_fit_prepared (engine.PreparedFit) == xpg_wlm_fit_from bit for
+    bit (w, losses, best epoch), twice on the same instance (the second prepare resets w / m / v
+    and the exchange slots), and two instances interleaved as the pipelined bench uses them."""
+    e = _eng()
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    g = torch.Generator().manual_seed(S)
+    fits = []
+    for s in range(2):
+        bits = e.sample_shapley(50 + s, R, S, DEV)
+        y = torch.rand(R, generator=g).to(DEV)
+        k = e.shap_kernel(bits, S)
+        w0 = (torch.rand((1, S), generator=g) - 0.5).to(DEV)
+        ref = e.wlm_fit(bits.view(1, R, -1), S, B, y.view(1, R), k.view(1, R), w0, params)
+        fits.append((bits, y, k, w0, ref))
+    pf = [e.PreparedFit(1, R, S, B, params, DEV), e.PreparedFit(1, R, S, B, params, DEV)]
+    for rep in range(2):
+        for i, (bits, y, k, w0, ref) in enumerate(fits):
+            pf[i].prepare(bits, y, k, w0)
+        for i, (bits, y, k, w0, ref) in enumerate(fits):
+            w = pf[i].fit(bits, k)
+            torch.cuda.synchronize()
+            e.check_fit_status(pf[i].status)
+            assert torch.equal(w, ref[0]), (rep, i)
+            assert torch.equal(pf[i].losses, ref[1]) and torch.equal(pf[i].best, ref[2])
+
+
 def test_captured_repeat_equals_eager():
     """One repeat (device-seeded masks -> masked forward, KernelSHAP on a side stream ->
     fresh surrogate fit) captured in a HIP graph, as bench.py's headline replays it: every
