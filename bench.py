@@ -244,6 +244,7 @@ def headline(args, dev, world, rank):
     split = world > 1 or os.environ.get("XPG_BENCH_SPLIT_GRAPH") == "1"
     # the pipelined graphs need each rank's fits to read only its own rows ((f0, f1) repeats
     # == rows [r0, r1), e.g. times = world): the fit must not regenerate rows from seed_t
+    unroll = 1
     pipe = use_graph and (f0 * R, f1 * R) == (r0, r1) and \
         os.environ.get("XPG_BENCH_PIPE", "1") == "1"
     split = split and not pipe
@@ -395,6 +396,15 @@ def headline(args, dev, world, rank):
                 with torch.cuda.graph(gph):
                     pipe_outs.append(pipe_step(i))
                 pipe_graphs.append(gph)
+            # one process: U consecutive pipelined steps in one graph (one launch per U steps
+            # instead of per step; the remainder of K replays the one-step graphs)
+            unroll = int(os.environ.get("XPG_BENCH_UNROLL", "1")) if world == 1 else 1
+            if unroll > 1:
+                unroll += unroll & 1  # even: the graph ends on the set parity it started on
+                unr_graph, unr_outs = torch.cuda.CUDAGraph(), []
+                with torch.cuda.graph(unr_graph):
+                    for j in range(unroll):
+                        unr_outs.append(pipe_step(j & 1))
         elif not split:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
@@ -418,7 +428,10 @@ def headline(args, dev, world, rank):
         torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    n_unr = args.steps // unroll if pipe and unroll > 1 else 0
+    for _ in range(n_unr):
+        unr_graph.replay()
+    for i in range(n_unr * (unroll if n_unr else 0), args.steps):
         if pipe:
             pipe_graphs[i & 1].replay()
             if world > 1:
@@ -435,7 +448,8 @@ def headline(args, dev, world, rank):
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
     graph_check = None
     if use_graph:  # outside the timed region: the last replay == an eager step on the same seed
-        last = (pipe_outs[(args.steps - 1) & 1] if world == 1 else out) if pipe else \
+        last = ((unr_outs[-1] if n_unr and n_unr * unroll == args.steps else pipe_outs[(args.steps - 1) & 1])
+                if world == 1 else out) if pipe else \
             out if split else g_out
         ref = step(args.warmup + args.steps - 1, False)
         graph_check = max(float((last[0] - ref[0]).abs().max()), float((last[1] - ref[1]).abs().max()))
@@ -486,7 +500,8 @@ def headline(args, dev, world, rank):
                               ("two captured HIP graphs per step (masks -> forward + KernelSHAP; "
                                "surrogate fit) with eager RCCL all-gathers between them"
                                if split else
-                              "two captured HIP graphs replayed alternately: step i's surrogate "
+                              f"pipelined captured HIP graphs ({unroll} step(s) per graph "
+                              "replay, XPG_BENCH_UNROLL): step i's surrogate "
                               "fit runs beside step i+1's masks -> forward + KernelSHAP "
                               "(double-buffered; the fit's prologue kernel runs with the "
                               "production; prologue untimed, K fits + K productions timed)"
