@@ -398,7 +398,7 @@ def headline(args, dev, world, rank):
                 pipe_graphs.append(gph)
             # one process: U consecutive pipelined steps in one graph (one launch per U steps
             # instead of per step; the remainder of K replays the one-step graphs)
-            unroll = int(os.environ.get("XPG_BENCH_UNROLL", "1")) if world == 1 else 1
+            unroll = int(os.environ.get("XPG_BENCH_UNROLL", "4")) if world == 1 else 1
             if unroll > 1:
                 unroll += unroll & 1  # even: the graph ends on the set parity it started on
                 unr_graph, unr_outs = torch.cuda.CUDAGraph(), []
