@@ -68,7 +68,7 @@ def parse():
                         "HIP graph per step")
     p.add_argument("--cpu-rows", type=int, default=12800)
     p.add_argument("--cpu-procs", type=int, default=0,
-                   help="CPU baseline worker processes (0: min(16, host cores))")
+                   help="CPU baseline worker processes (0: every usable host core)")
     p.add_argument("--c3-rows", type=int, default=512,
                    help="regime (ii): mask rows of the c3 full-graph forward (all ranks)")
     p.add_argument("--c5-times", type=int, default=10)
@@ -77,23 +77,61 @@ def parse():
 
 
 # ----------------------------------------------------------------------------- plumbing
-def setup_dist():
+def launch_ranks(args):
+    """`--gpus N > 1` without a torch.distributed environment: start N ranks (one process per GPU,
+    RCCL) with torch.distributed.run as a CHILD process and return its exit code.  Called before
+    anything touches the GPU; rank 0 of the child prints the JSON line."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: launch one rank per "
+                         "GPU (python bench.py --gpus N starts them itself)")
     if world > 1:
         import torch.distributed as dist
         # XPG_BENCH_BACKEND=gloo + XPG_BENCH_ONE_GPU=1: a rehearsal of the N-rank path with
         # every rank on cuda:0 (one-GPU box); the driver's runs use RCCL, one GPU per rank
         if os.environ.get("XPG_BENCH_ONE_GPU") == "1":
             local = 0
+        elif local >= torch.cuda.device_count():
+            raise SystemExit(f"bench: rank {rank} has local rank {local} but only "
+                             f"{torch.cuda.device_count()} GPU(s) are visible")
         torch.cuda.set_device(local)
         backend = os.environ.get("XPG_BENCH_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)}
                                             if backend == "nccl" else {}))
+        assert dist.get_world_size() == args.gpus
     else:
         torch.cuda.set_device(0)
     return world, rank, local
+
+
+def rank_layout(world, local):
+    """Backend, world size and every rank's device (index + PCI bus) — gathered once, untimed."""
+    props = torch.cuda.get_device_properties(local)
+    me = {"local_rank": local, "device": local, "name": props.name,
+          "pci_bus_id": getattr(props, "pci_bus_id", None), "host": platform.node()}
+    if world == 1:
+        return {"backend": None, "world": 1, "ranks": [me]}
+    import torch.distributed as dist
+    ranks = [None] * world
+    dist.all_gather_object(ranks, me)
+    backend = dist.get_backend()
+    return {"backend": "nccl (RCCL)" if backend == "nccl" else backend, "world": world,
+            "ranks": ranks, "distinct_devices": len({(r["host"], r["pci_bus_id"], r["device"])
+                                                     for r in ranks})}
 
 
 def barrier(world):
@@ -131,8 +169,27 @@ def host_info():
     return model, os.cpu_count()
 
 
-def cpu_procs(args):
-    return args.cpu_procs or max(1, min(16, os.cpu_count() or 1))
+def host_cores():
+    """(usable, detail): the CPUs this job may run on — the affinity mask, capped by the cgroup
+    CPU quota (a GPU box shows every CPU of the machine in os.cpu_count(), but schedules this
+    job on its share)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    n = max(1, min(aff, int(quota)) if quota else aff)
+    return n, {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+
+
+def cpu_procs(args, cap=None):
+    """CPU baseline worker processes: every usable host core (--cpu-procs overrides); `cap`
+    bounds memory-heavy workers."""
+    n = args.cpu_procs or host_cores()[0]
+    return max(1, min(n, cap) if cap else n)
 
 
 def _pool(n):
@@ -236,10 +293,10 @@ def headline(args, dev, world, rank):
     ev = {k: [] for k in phases}
     # The step is host-launch-bound in eager mode (~55 us of GPU idle per 0.3 ms step in the
     # kernel trace), so it is replayed from captured HIP graphs: the sampler reads its seed from
-    # device memory and the graph advances it, so every replay draws new mask rows.  One
-    # process: ONE graph per step.  Several ranks: the RCCL all-gathers stay eager between two
-    # graphs (A: masks -> forward + KernelSHAP; B: the surrogate fit), nothing collective is
-    # captured (XPG_BENCH_SPLIT_GRAPH=1 runs this split form on one GPU too).
+    # device memory and the graph advances it, so every replay draws new mask rows.  Default:
+    # the pipelined graphs (below).  XPG_BENCH_PIPE=0: ONE graph per step (one process), or the
+    # split form with eager RCCL all-gathers between two graphs (several ranks, or
+    # XPG_BENCH_SPLIT_GRAPH=1).
     use_graph = not args.no_graph
     split = world > 1 or os.environ.get("XPG_BENCH_SPLIT_GRAPH") == "1"
     # the pipelined graphs need each rank's fits to read only its own rows ((f0, f1) repeats
@@ -252,6 +309,7 @@ def headline(args, dev, world, rank):
     k_buf = torch.empty(r1 - r0, dtype=torch.float64, device=dev)
     stash = {}
     cnt_buf = torch.empty(r1 - r0, dtype=torch.int32, device=dev)
+    exchange = None
 
     def part_a(seed, dev_seed, mk=lambda j: None):
         """masks -> forward (+ KernelSHAP on the side stream): this rank's rows"""
@@ -288,7 +346,7 @@ def headline(args, dev, world, rank):
             fbits = engine.sample_shapley_dev(seed_t, (f1 - f0) * R, S, row_offset=f0 * R)
         else:
             fbits = engine.sample_shapley(seed, (f1 - f0) * R, S, dev, row_offset=f0 * R)
-        st = torch.empty(1, dtype=torch.int32, device=dev)
+        st = torch.zeros(1, dtype=torch.int32, device=dev)
         w, _, _, _, _ = engine.wlm_fit(fbits.view(f1 - f0, R, -1), S, batch,
                                        y[f0 * R:f1 * R].view(f1 - f0, R),
                                        k[f0 * R:f1 * R].view(f1 - f0, R), w0[f0:f1], params,
@@ -323,6 +381,7 @@ def headline(args, dev, world, rank):
 
     for i in range(args.warmup):
         step(i, False)
+    results = []
     if use_graph:
         # the phase breakdown comes from 3 eager steps outside the timed region (events cannot
         # split a graph replay); then one eager dev-seed step and the capture
@@ -332,79 +391,86 @@ def headline(args, dev, world, rank):
         seed_t.fill_(1000 + args.warmup)
         torch.cuda.synchronize()
         if pipe:
-            # two graphs, ping-pong over two static sets of (bits, y, k): graph i fits the repeat
-            # in set i (capture stream) while the NEXT repeat's masks -> forward + KernelSHAP
-            # fill set 1 - i on side streams (allocation-free).  The fit is latency-bound on a
-            # few workgroups, the forward fills the rest of the chip.  Prologue (untimed): the
-            # first repeat's set; the timed K replays do K fits + K productions.
-            # Several ranks: each graph holds the fit + this rank's rows of the next repeat; the
-            # RCCL all-gathers of the next repeat's logits / kernel weights and the weight
-            # stacking stay eager after the replay (nothing collective is captured).
-            W_, nl = (S + 31) // 32, r1 - r0
+            # Pipelined graphs over two static buffer sets (bits, y, k and a PreparedFit each):
+            # global step i fits the repeat in set i & 1 on the capture stream while the next
+            # repeat's masks -> forward -> KernelSHAP -> fit prologue fill set 1 - (i & 1) on a
+            # side stream (allocation-free).  The fit is latency-bound on a few workgroups, the
+            # production fills the rest of the chip beside it.  Every rank fits its own repeats
+            # (rows [r0, r1) are repeats [f0, f1)), which it produced itself, so no fit waits
+            # for a collective.  Several ranks: each step's logits, kernel weights (copied on
+            # the side stream) and fitted weights (after the fit) go to a staging row; ONE RCCL
+            # all-gather per graph replay, issued asynchronously right after it, exchanges the
+            # replay's rows.  The host never waits: the stream waits for that exchange only
+            # before the replay that rewrites its staging buffer (two replays later), and the
+            # mean / std over all ranks' repeats (weight_stacking) of those steps runs then.
+            # A graph holds U consecutive steps (XPG_BENCH_UNROLL, default 4: one launch and one
+            # exchange per U steps; U = 1 or even, dividing --steps).  Prologue (untimed): the
+            # first repeat's production; the K timed steps do K fits + K productions.
+            W_, nl, nf = (S + 31) // 32, r1 - r0, f1 - f0
             sets = []
             for _ in range(2):
                 d = dict(bits=torch.empty((nl, W_), dtype=torch.int32, device=dev),
                          y=torch.empty((nl, plan.n_out), dtype=torch.float32, device=dev),
                          k=torch.empty(nl, dtype=torch.float64, device=dev),
-                         cnt=torch.empty(nl, dtype=torch.int32, device=dev))
-                d["yf"] = torch.empty(n_rows, dtype=torch.float32, device=dev) if world > 1 \
-                    else d["y"][:, 0]
-                d["kf"] = torch.empty(n_rows, dtype=torch.float64, device=dev) if world > 1 \
-                    else d["k"]
+                         cnt=torch.empty(nl, dtype=torch.int32, device=dev),
+                         fit=engine.PreparedFit(nf, R, S, batch, params, dev))
+                statuses.append(d["fit"].status)
                 sets.append(d)
             s1 = torch.cuda.Stream(device=dev)
-
-            # one process: the fit's prologue (xpg_wlm_prepare, own workspace per set) runs in
-            # the production branch too, so the fit branch is the Adam steps alone
-            pre = world == 1 and sets[0]["yf"].is_contiguous() and \
-                os.environ.get("XPG_BENCH_PREPARE", "1") == "1"
-            if pre:
-                for d in sets:
-                    d["fit"] = engine.PreparedFit(1, R, S, batch, params, dev)
-                    statuses.append(d["fit"].status)
+            want = max(1, int(os.environ.get("XPG_BENCH_UNROLL", "4")))
+            unroll = next((u for u in range(want, 1, -1) if u % 2 == 0 and args.steps % u == 0), 1)
+            ex = world > 1
+            if ex:  # staging row: y fp32 [nl] | k fp64 [nl] | w fp32 [nf, S]
+                oy, ok_ = 0, -(-nl * 4 // 8) * 8
+                ow = ok_ + nl * 8
+                sb = -(-(ow + nf * S * 4) // 16) * 16
+                stage = [torch.zeros((unroll, sb), dtype=torch.uint8, device=dev) for _ in range(2)]
+                gath = [torch.zeros((world, unroll, sb), dtype=torch.uint8, device=dev)
+                        for _ in range(2)]
 
             def produce(d):  # (in order on its stream: it is off the fit's critical path)
                 engine.sample_shapley_dev(seed_t, nl, S, row_offset=r0, out=d["bits"])
                 seed_t.add_(1)
                 plan.forward(d["bits"], out=d["y"])
                 engine.shap_kernel(d["bits"], S, out=d["k"], scratch=d["cnt"])
-                if pre:
-                    d["fit"].prepare(d["bits"], d["yf"], d["kf"], w0)
+                d["fit"].prepare(d["bits"], d["y"][:, 0], d["k"], w0[f0:f1])
 
-            def exchange(d):  # eager RCCL all-gathers of a produced set (several ranks)
-                if world > 1:
-                    d["yf"].copy_(sharding.gather_rows(d["y"][:, 0], n_rows))
-                    d["kf"].copy_(sharding.gather_rows(d["k"], n_rows))
-
-            def pipe_step(i):
+            def pipe_step(i_set, row):
                 cur = torch.cuda.current_stream()
                 s1.wait_stream(cur)
-                w = sets[i]["fit"].fit(sets[i]["bits"], sets[i]["kf"]) if pre else \
-                    part_b(0, True, sets[i]["bits"], sets[i]["yf"], sets[i]["kf"])
-                out = part_c(w) if world == 1 else w
+                d = sets[i_set]
+                w = d["fit"].fit(d["bits"], d["k"])
+                out = None
+                if row is None:
+                    out = part_c(w)
+                else:
+                    row[ow:ow + nf * S * 4].view(torch.float32).copy_(w.reshape(-1))
                 with torch.cuda.stream(s1):
-                    produce(sets[1 - i])
+                    if row is not None:  # this step's repeat: logits + kernel weights
+                        row[oy:oy + nl * 4].view(torch.float32).copy_(d["y"][:, 0])
+                        row[ok_:ok_ + nl * 8].view(torch.float64).copy_(d["k"])
+                    produce(sets[1 - i_set])
                 cur.wait_stream(s1)
                 return out
 
+            def stacked(b):  # mean / std over all ranks' repeats of replay buffer b's U steps
+                w_all = gath[b][:, :, ow:ow + nf * S * 4].contiguous().view(torch.float32)
+                w_all = w_all.view(world, unroll, nf, S).transpose(0, 1).reshape(unroll, world * nf, S)
+                std, mean = torch.std_mean(w_all, 1, unbiased=False)
+                return [(mean[j], std[j]) for j in range(unroll)]
+
             produce(sets[0])  # prologue: the first timed step's repeat
-            exchange(sets[0])
             torch.cuda.synchronize()
-            pipe_graphs, pipe_outs = [], []
-            for i in range(2):
-                gph = torch.cuda.CUDAGraph()
+            graphs = []
+            for b in range(2):
+                gph, outs = torch.cuda.CUDAGraph(), []
                 with torch.cuda.graph(gph):
-                    pipe_outs.append(pipe_step(i))
-                pipe_graphs.append(gph)
-            # one process: U consecutive pipelined steps in one graph (one launch per U steps
-            # instead of per step; the remainder of K replays the one-step graphs)
-            unroll = int(os.environ.get("XPG_BENCH_UNROLL", "4")) if world == 1 else 1
-            if unroll > 1:
-                unroll += unroll & 1  # even: the graph ends on the set parity it started on
-                unr_graph, unr_outs = torch.cuda.CUDAGraph(), []
-                with torch.cuda.graph(unr_graph):
                     for j in range(unroll):
-                        unr_outs.append(pipe_step(j & 1))
+                        outs.append(pipe_step((b * unroll + j) & 1, stage[b][j] if ex else None))
+                graphs.append((gph, outs))
+
+            def exchange(b):
+                return sharding.all_gather_async(gath[b].view(-1), stage[b].view(-1))
         elif not split:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
@@ -428,32 +494,48 @@ def headline(args, dev, world, rank):
         torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
-    n_unr = args.steps // unroll if pipe and unroll > 1 else 0
-    for _ in range(n_unr):
-        unr_graph.replay()
-    for i in range(n_unr * (unroll if n_unr else 0), args.steps):
-        if pipe:
-            pipe_graphs[i & 1].replay()
-            if world > 1:
-                exchange(sets[1 - (i & 1)])
-                out = part_c(pipe_outs[i & 1])
-        elif use_graph and not split:
-            graph.replay()
-        elif use_graph:
-            out = split_step()
-        else:
-            step(args.warmup + i, True)
+    if pipe:
+        pending = [None, None]
+        for m in range(args.steps // unroll):
+            b = m & 1
+            if pending[b] is not None:  # replay m - 2's exchange: before its buffer is rewritten
+                pending[b].wait()
+                results += stacked(b)
+            graphs[b][0].replay()
+            if ex:
+                pending[b] = exchange(b)
+        for m in range(max(0, args.steps // unroll - 2), args.steps // unroll):
+            if pending[m & 1] is not None:
+                pending[m & 1].wait()
+                results += stacked(m & 1)
+    else:
+        for i in range(args.steps):
+            if use_graph and not split:
+                graph.replay()
+            elif use_graph:
+                results.append(split_step())
+            else:
+                step(args.warmup + i, True)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world, dev)
-    graph_check = None
-    if use_graph:  # outside the timed region: the last replay == an eager step on the same seed
-        last = ((unr_outs[-1] if n_unr and n_unr * unroll == args.steps else pipe_outs[(args.steps - 1) & 1])
-                if world == 1 else out) if pipe else \
-            out if split else g_out
+    graph_check = exchange_check = None
+    if use_graph:  # outside the timed region: the last step == an eager step on the same seed
+        if pipe:
+            last = results[-1] if ex else graphs[(args.steps // unroll - 1) & 1][1][-1]
+        else:
+            last = results[-1] if split else g_out
         ref = step(args.warmup + args.steps - 1, False)
         graph_check = max(float((last[0] - ref[0]).abs().max()), float((last[1] - ref[1]).abs().max()))
-        if os.environ.get("XPG_BENCH_DEBUG"):
+        if pipe and ex:
+            # this rank's staged slot of the last exchange == its last fitted repeat's
+            # logits / kernel weights (every rank checks its own slot; max over ranks)
+            bl, d = (args.steps // unroll - 1) & 1, sets[(args.steps - 1) & 1]
+            mine = gath[bl][rank, unroll - 1]
+            exchange_check = max_over_ranks(max(
+                float((mine[oy:oy + nl * 4].view(torch.float32) - d["y"][:, 0]).abs().max()),
+                float((mine[ok_:ok_ + nl * 8].view(torch.float64) - d["k"]).abs().max())), world, dev)
+        if os.environ.get("XPG_BENCH_DEBUG") and not pipe:
             sd = 1000 + args.warmup + args.steps - 1
             b_e = engine.sample_shapley(sd, r1 - r0, S, dev, row_offset=r0)
             y_e = plan.forward(b_e)[:, 0]
@@ -463,11 +545,7 @@ def headline(args, dev, world, rank):
                 g = stash[nm]
                 log(rank, f"stage {nm}: max|diff| {float((g.double() - e.double()).abs().max()):.3e} "
                           f"nan {int(torch.isnan(g.double()).sum())} shape {tuple(g.shape)} vs {tuple(e.shape)}")
-            log(rank, f"status {int(stash['st'].item())} seed_t {int(seed_t.item())}")
-            log(rank, f"graph check: nan last {int(torch.isnan(last[0]).sum())}/{int(torch.isnan(last[1]).sum())} "
-                      f"ref {int(torch.isnan(ref[0]).sum())}/{int(torch.isnan(ref[1]).sum())} "
-                      f"last[:4] {last[0][:4].tolist()} ref[:4] {ref[0][:4].tolist()}")
-    for st in statuses:  # outside the timed region: every fit's exchange status must be clean
+    for st in statuses:  # outside the timed region: every fit's (sticky) exchange status
         engine.check_fit_status(st)
     phase_ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in ev.items()}
     total_rows = n_rows * args.steps
@@ -492,10 +570,15 @@ def headline(args, dev, world, rank):
                    "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
                    "interpret_samples": args.interpret_samples, "epochs": args.epochs,
                    "rows_per_repeat": R, "repeats_per_step": times,
-                   "parallelism": f"dp{world}: rows of the step's {times} repeat(s) sharded over "
+                   "parallelism": f"dp{world}: one repeat per rank per step (its rows and its "
+                                  "fit); per graph replay one async RCCL all-gather of the "
+                                  "replay's logits, kernel weights and fitted weights, then "
+                                  "mean / std over all ranks' repeats" if pipe and world > 1 else
+                                  f"dp{world}: rows of the step's {times} repeat(s) sharded over "
                                   "ranks, RCCL all-gather of logits + kernel weights, fits "
                                   "sharded by repeat",
                    "mask_sampler": "device (Philox Shapley)",
+                   "surrogate_fit": "%s (%d workgroup(s) per fit)" % engine.wlm_plan(f1 - f0, R, S, batch),
                    "launch": ("eager" if not use_graph else
                               ("two captured HIP graphs per step (masks -> forward + KernelSHAP; "
                                "surrogate fit) with eager RCCL all-gathers between them"
@@ -510,6 +593,8 @@ def headline(args, dev, world, rank):
                               "phases_ms from eager steps")},
         "phases_ms": phase_ms,
         "graph_check_max_abs_diff": graph_check,
+        "exchange_check_max_abs_diff": exchange_check,
+        "fit_status": "clean (sticky status words of every fit checked after the timed region)",
         "roofline": dict(roofline(wl, phase_ms["wlm"] * 1e-3, "headline", WLM_KERNELS),
                          kernel="surrogate fit chain (" + ", ".join(WLM_KERNELS) + ")",
                          note="latency-bound (51 sequential Adam steps, SURVEY.md §8d regime "
@@ -558,7 +643,7 @@ def cpu_baseline_c2(args, arch, sub_feat, sub_ei, q):
         dt = time.perf_counter() - t0
     model, ncpu = host_info()
     return {"value": rows / dt, "unit": "samples/s", "cores": procs, "kind": "port",
-            "host_cpu": model, "host_logical_cpus": ncpu,
+            "host_cpu": model, "host_logical_cpus": ncpu, "host_cores": host_cores()[1],
             "sample": f"{rows} mask rows of the same workload (S={S}) through the numpy oracle: "
                       f"union-graph forward over {procs} worker processes (1 thread each), "
                       f"KernelSHAP, surrogate fit; {dt:.1f} s"}
@@ -699,14 +784,14 @@ def _c3_cpu_worker(seed):
 def cpu_baseline_c3(args):
     """The numpy oracle on the host cores: one full-size c3 mask row (1M nodes / 10M edges, every
     node an output) per worker process, all workers at once."""
-    procs = cpu_procs(args)
+    procs = cpu_procs(args, cap=48)  # each worker regenerates the 1M / 10M graph (~2 GB)
     with _pool(procs) as pool:
         t0 = time.perf_counter()
         per = pool.map(_c3_cpu_worker, list(range(procs)))
         dt = time.perf_counter() - t0
     model, ncpu = host_info()
     return {"value": procs / max(per), "unit": "samples/s", "cores": procs, "kind": "port",
-            "host_cpu": model, "host_logical_cpus": ncpu,
+            "host_cpu": model, "host_logical_cpus": ncpu, "host_cores": host_cores()[1],
             "sample": f"{procs} full-size mask rows, one per worker process (1 thread each, all "
                       f"concurrent), through the numpy oracle's union-graph forward: "
                       f"{np.mean(per):.1f} s mean / {max(per):.1f} s max forward per row "
@@ -1096,10 +1181,13 @@ def graph_queries_section(args, dev, n=10_000, e=100_000, f=64, queries=8):
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
-    world, rank, local = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world, rank, local = setup_dist(args)
     dev = torch.device("cuda", torch.cuda.current_device())
     from bikg_graph_explainability_public_amd import _lib
     _lib.load()
+    layout = rank_layout(world, local)
     want = SECTIONS if args.sections == "all" else tuple(args.sections.split(","))
     if world > 1:
         want = tuple(s for s in want if s in MULTI_GPU_SECTIONS)
@@ -1124,6 +1212,7 @@ def main():
             log(rank, f"section {name} done in {time.perf_counter() - t0:.1f} s")
     if regimes:
         line["regimes"] = regimes
+    line["rank_layout"] = layout
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

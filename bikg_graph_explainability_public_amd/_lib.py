@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -82,6 +82,7 @@ _SIGS = {
     "xpg_masked_forward": ([ctypes.POINTER(ForwardPlanDesc), c_vp, c_i64, c_vp, c_vp,
                             ctypes.c_size_t, c_vp], c_i32),
     "xpg_wlm_workspace": ([c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)], c_i32),
+    "xpg_wlm_plan": ([c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)], c_i32),
     "xpg_wlm_fit": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, ctypes.POINTER(WlmParams), c_i64,
                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
     "xpg_wlm_fit_from": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, ctypes.POINTER(WlmParams), c_vp,

@@ -3836,7 +3836,10 @@ __global__ __launch_bounds__(256) void k_wlm_loss_best(const float* __restrict__
   __shared__ double red[16];
   __shared__ int last_s;
   const int64_t t = blockIdx.x, f = blockIdx.y, steps = gridDim.x;
-  if (status && f == 0 && t == 0 && threadIdx.x == 0) *status = errw ? static_cast<int32_t>(*errw) : 0;
+  // sticky: OR the exchange's error word into the caller's word (zeroed once by the caller), so
+  // a timeout in any fit of a replayed chain stays visible after the last one (ABI v13)
+  if (status && errw && f == 0 && t == 0 && threadIdx.x == 0 && *errw)
+    *status = *status | static_cast<int32_t>(*errw);
   p_hist += f * rows;
   w_hist += f * steps * cols;
   kern += f * rows;
@@ -4152,7 +4155,7 @@ __global__ __launch_bounds__(64) void k_gw_loss(const double* __restrict__ tk_pa
 __global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t* __restrict__ out,
                                const uint32_t* __restrict__ errw, int32_t* __restrict__ status) {
   if (threadIdx.x != 0) return;
-  if (status && blockIdx.x == 0) *status = errw ? static_cast<int32_t>(*errw) : 0;
+  if (status && errw && blockIdx.x == 0 && *errw) *status = *status | static_cast<int32_t>(*errw);
   v += blockIdx.x * n;
   out += blockIdx.x;
   double best = INFINITY;
@@ -5283,6 +5286,16 @@ int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
   int rc = wlm_layout(n_fits, rows, cols, batch, &L);
   if (rc) return rc;
   *bytes = L.total;
+  return XPG_OK;
+}
+
+int xpg_wlm_plan(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, int32_t* kind, int32_t* parts) {
+  XPG_REQ(kind != nullptr && parts != nullptr, "wlm_plan: null output");
+  WlmWs L;
+  int rc = wlm_layout(n_fits, rows, cols, batch, &L);
+  if (rc) return rc;
+  *kind = L.grid ? XPG_WLM_GRID : (L.mc ? XPG_WLM_MULTI : XPG_WLM_SINGLE);
+  *parts = L.mc && !L.grid ? L.P : 1;
   return XPG_OK;
 }
 

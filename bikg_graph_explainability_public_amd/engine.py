@@ -524,15 +524,34 @@ def check_fit_status(status):
             "XPG_WLM=single selects the single-workgroup fit.")
 
 
+WLM_KINDS = {0: "single", 1: "multi", 2: "grid"}
+
+
+def wlm_plan(n_fits, rows, cols, batch):
+    """(kind, parts) of the fit kernel a shape takes on the current device (xpg_wlm_plan):
+    kind "single" (one workgroup per fit), "multi" (`parts` co-resident workgroups per fit) or
+    "grid" (the many-column streaming fit, which has no prepared form)."""
+    kind, parts = ctypes.c_int32(0), ctypes.c_int32(0)
+    _lib.check(_lib.load().xpg_wlm_plan(int(n_fits), int(rows), int(cols), int(batch),
+                                        ctypes.byref(kind), ctypes.byref(parts)))
+    return WLM_KINDS[kind.value], parts.value
+
+
 class PreparedFit:
     """A fresh surrogate fit (`wlm_fit` from w0) split in its two launches on static buffers of
     one shape (xpg_wlm_prepare / xpg_wlm_fit_prepared, ABI v12): `prepare` runs the prologue
     (per-step constants, column bit vectors, w = w0, zero Adam moments), `fit` the Adam steps and
     returns w [F, cols].  Nothing is allocated after construction, so both can be captured on
     any stream; with two instances the next fit is prepared while the current one runs.
-    `status` is the device status word (check_fit_status)."""
+    `status` is the device status word (check_fit_status; sticky over every fit of the
+    instance).  Shapes that take the many-column grid fit have no prepared form: ValueError at
+    construction (use wlm_fit)."""
 
     def __init__(self, n_fits, rows, cols, batch, params, device):
+        self.kind, self.parts = wlm_plan(n_fits, rows, cols, batch)
+        if self.kind == "grid":
+            raise ValueError(f"PreparedFit: {cols} columns take the many-column grid fit, which "
+                             "has no prologue / prepared form; use wlm_fit")
         self.shape = (int(n_fits), int(rows), int(cols), int(batch))
         n = ctypes.c_size_t(0)
         _lib.check(_lib.load().xpg_wlm_workspace(n_fits, rows, cols, batch, ctypes.byref(n)))
@@ -579,7 +598,8 @@ def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0,
 
     check=True reads the fit's status word and raises FitExchangeError if the multi-workgroup
     exchange failed (one stream sync).  check=False leaves that to the caller: pass `status`
-    (device int32 [1]) and call check_fit_status(status) later (e.g. after a timed region)."""
+    (device int32 [1], zeroed once) and call check_fit_status(status) later (e.g. after a timed
+    region); the word is sticky (ABI v13), so it reports a failure of any fit that used it."""
     dev = bits.device
     batched = bits.dim() == 3
     F = bits.shape[0] if batched else 1
@@ -612,8 +632,8 @@ def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0,
     n = ctypes.c_size_t(0)
     _lib.check(_lib.load().xpg_wlm_workspace(F, rows, cols, batch, ctypes.byref(n)))
     ws = _workspace(dev, n.value)
-    if status is None:
-        status = torch.empty(1, dtype=torch.int32, device=dev)
+    if status is None:  # sticky word (the fit ORs its error into it): starts at 0
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
     if fresh:
         call("xpg_wlm_fit_from", F, ptr(bb), rows, cols, batch, ptr(yy), ptr(kk), ctypes.byref(p),
              ptr(w0f), ptr(w), ptr(m), ptr(v), ptr(losses), ptr(best), ptr(status), ptr(ws),

@@ -118,6 +118,32 @@ def gather_rows(local, n, group=None):
     return torch.cat(parts, 0).to(local.device)
 
 
+class _Done:
+    """Handle of an exchange that already completed (gloo rehearsal)."""
+
+    def wait(self):
+        return True
+
+
+def all_gather_async(out, inp, group=None):
+    """out [world * n, ...] <- every rank's inp [n, ...] (equal shard sizes), rank-major, without
+    a host sync: RCCL returns a work handle whose wait() makes the CURRENT stream wait for the
+    exchange (the host never blocks), so a caller can overlap it with the next step and wait
+    only before it overwrites `inp` or reads `out`.  gloo (CPU test backend; GPU tensors go
+    through host copies): synchronous, returns a finished handle."""
+    import torch.distributed as dist
+    world, _ = world_info(group)
+    if out.numel() != world * inp.numel():
+        raise ValueError(f"all_gather_async: out holds {out.numel()} elements, expected "
+                         f"{world} x {inp.numel()}")
+    if dist.get_backend(group) == "gloo" and inp.device.type != "cpu":
+        ob = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(ob, inp.cpu().contiguous(), group=group)
+        out.copy_(ob)
+        return _Done()
+    return dist.all_gather_into_tensor(out, inp.contiguous(), group=group, async_op=True)
+
+
 def gather_map(n, fn, group=None):
     """Run `fn(start, stop)` on this rank's shard of n units and all-gather the results.
 

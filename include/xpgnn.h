@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 12
+#define XPG_ABI_VERSION 13
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -199,14 +199,23 @@ typedef struct xpg_wlm_params {
 
 /* Workspace needed by xpg_wlm_fit. */
 int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, size_t* bytes);
+/* Which fit kernel a shape takes (v13): *kind = XPG_WLM_SINGLE (one workgroup per fit),
+ * XPG_WLM_MULTI (*parts co-resident workgroups per fit) or XPG_WLM_GRID (the many-column
+ * streaming fit: no xpg_wlm_prepare / xpg_wlm_fit_prepared); *parts = 1 unless MULTI.  The
+ * choice depends on the current device's CU count and the XPG_WLM / XPG_MC_* overrides. */
+enum xpg_wlm_kind { XPG_WLM_SINGLE = 0, XPG_WLM_MULTI = 1, XPG_WLM_GRID = 2 };
+int xpg_wlm_plan(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, int32_t* kind,
+                 int32_t* parts);
 /* Runs ceil(rows / batch) Adam steps of train_model over consecutive row batches for n_fits
  * independent surrogates (e.g. the `times` repeats of Explainer.run), one workgroup each.
  * Arrays are fit-major and contiguous: bits [n_fits][rows][words], y / kernel [n_fits][rows],
  * w / adam_m / adam_v [n_fits][cols] (updated in place), losses [n_fits][steps] (fp64),
  * best_epoch [n_fits] (first argmin).  `step0` = Adam steps already taken with (m, v).
- * status (device int32 [1], nullable): 0 once the stream reaches the end of the fit, nonzero
- * if the multi-workgroup fit's cross-workgroup exchange timed out (a partner workgroup was not
- * co-resident) — every output of the call is then invalid and the caller must not use it. */
+ * status (device int32 [1], nullable, zeroed by the caller): sticky — the call ORs a nonzero
+ * error word into it when the multi-workgroup fit's cross-workgroup exchange timed out (a
+ * partner workgroup was not co-resident) and never clears it (v13), so one word checked after
+ * many fits (e.g. K replays of a captured chain) reports a failure in any of them; every
+ * output of a failed call is invalid and the caller must not use it. */
 int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols,
                 int64_t batch, const float* y, const double* kernel,
                 const xpg_wlm_params* params, int64_t step0, float* w, float* adam_m,

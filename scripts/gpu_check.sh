@@ -19,6 +19,19 @@ for step in "$@"; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py ;;
     bench10) run bench10 600 python bench.py --repeats 10 --no-cpu-baseline ;;
+    headline) run headline 300 python bench.py --sections headline --no-cpu-baseline ;;
+    repeats2) run repeats2 300 python bench.py --repeats 2 --sections headline --no-cpu-baseline ;;
+    # bench.py --gpus 2 launches its own ranks (torch.distributed.run child); gloo rehearsal with
+    # both ranks on cuda:0 (the driver's 8-GPU runs use RCCL, one GPU per rank)
+    rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
+    capture) run capture 400 python tools/capture_probe.py ;;
+    # layer-2 ablations (c3 full size, one 32-row pass): full, no MFMA, no gathers, no epilogue,
+    # exact f32 (B3=0) beside the default bf16x3
+    wsdbg) run wsdbg 500 python tools/ws_ab.py --variants "B3=1;B3=1,DBG=16;B3=1,DBG=32;B3=1,DBG=64;B3=0" ;;
+    # FETCH_SIZE / WRITE_SIZE factors per access shape (tools/fetch_calib.hip, known bytes)
+    calib) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/calib_fetch -o run -- ./tools/fetch_calib && \
+           run calib_write 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/calib_write -o run -- ./tools/fetch_calib ;;
     fwdprobe) XPG_LIB=tools/libxpgnn_stamps.so run fwdprobe 300 python tools/fwd_probe.py ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;
     profall) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \

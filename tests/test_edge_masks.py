@@ -88,6 +88,32 @@ def test_perturb_edge_known_answer():
     np.testing.assert_array_equal(et, [7, 9, 8, 9])
 
 
+# the reference's own vector (tests/test_data.py:1907-1990): 7 nodes, 6 typed edges, a FLAT
+# 18-entry mask with entries 1 and 4 set -> [[2, 4], [6, 2]], types [0, 1]
+REF_PE_EI = np.array([[0, 2, 3, 6, 4, 5], [5, 6, 4, 1, 2, 0]])
+REF_PE_ET = np.array([0, 0, 0, 1, 1, 1])
+REF_PE_MASK = np.zeros(18, dtype=bool)
+REF_PE_MASK[[1, 4]] = True
+REF_PE_OUT = (np.array([[2, 4], [6, 2]]), np.array([0, 1]))
+
+
+def test_perturb_edge_reference_vector():
+    """The reference's test_perturb_edge vector through the oracle and the package's
+    Data.perturb_edge (CPU tensors): the flat mask tiles mask.shape[0] = 18 copies."""
+    from bikg_graph_explainability_public_amd.data import Data
+    pei, et = oracle.perturb_edge(REF_PE_MASK, REF_PE_EI, 7, edge_type=REF_PE_ET)
+    np.testing.assert_array_equal(pei, REF_PE_OUT[0])
+    np.testing.assert_array_equal(et, REF_PE_OUT[1])
+    d = Data(torch.zeros(7, 4), torch.from_numpy(REF_PE_EI).int())
+    pei_t, et_t = d.perturb_edge(torch.from_numpy(REF_PE_MASK), torch.from_numpy(REF_PE_ET).int())
+    np.testing.assert_array_equal(pei_t.numpy(), REF_PE_OUT[0])
+    np.testing.assert_array_equal(et_t.numpy(), REF_PE_OUT[1])
+    # a 2-D mask of the same 18 entries ([3, 6]: three copies) keeps the same two columns
+    pei2, et2 = oracle.perturb_edge(REF_PE_MASK.reshape(3, 6), REF_PE_EI, 7, edge_type=REF_PE_ET)
+    np.testing.assert_array_equal(pei2, REF_PE_OUT[0])
+    np.testing.assert_array_equal(et2, REF_PE_OUT[1])
+
+
 def test_plan_arrays_edge_columns():
     """Edge-mask CSRs carry each entry's mask column; self-loops go to the self CSR."""
     from bikg_graph_explainability_public_amd.engine import plan_arrays
@@ -157,6 +183,35 @@ def test_engine_edge_forward_vs_oracle(_gpu, kind, dims, fc, query):
     ok, err = pipeline.verify_edge_plan(plan, model, torch.from_numpy(x).to(DEV),
                                         torch.from_numpy(ei).to(DEV), u, v)
     assert ok, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["gcn", "sage"])
+def test_reference_perturb_edge_vector_on_device(_gpu, kind):
+    """The reference's test_perturb_edge vector (tests/test_data.py:1907-1990) on the device:
+    Data.perturb_edge of the flat 18-entry mask on device tensors, and the HIP edge-mask plan on
+    the same 18 entries read as 3 rows x 6 edges (row 0 keeps edges 1 and 4, rows 1-2 keep
+    none) vs the oracle's perturb_edge union-graph forward, with the reference's feature rows."""
+    from bikg_graph_explainability_public_amd import engine, pipeline
+    from bikg_graph_explainability_public_amd.data import Data
+    x = np.array([[0.24, 0.56, 0.96, 0.54], [0.78, 0.96, 0.12, 0.19], [0.85, 0.91, 0.92, 0.13],
+                  [1.91, 0.98, 0.54, 0.21], [0.97, 0.23, 0.0, 0.0], [0.21, 0.24, 0.0, 0.0],
+                  [0.29, 0.37, 0.0, 0.0]], dtype=np.float32)
+    d = Data(torch.from_numpy(x).to(DEV), torch.from_numpy(REF_PE_EI).int().to(DEV))
+    pei, et = d.perturb_edge(torch.from_numpy(REF_PE_MASK).to(DEV),
+                             torch.from_numpy(REF_PE_ET).int().to(DEV))
+    np.testing.assert_array_equal(pei.cpu().numpy(), REF_PE_OUT[0])
+    np.testing.assert_array_equal(et.cpu().numpy(), REF_PE_OUT[1])
+    dims, fc = [4, 8, 8], [8]
+    model = _link(kind, dims, fc).to(DEV)
+    u, v = int(REF_PE_EI[0, 1]), int(REF_PE_EI[1, 1])
+    plan = pipeline.build_edge_plan(model, torch.from_numpy(x).to(DEV),
+                                    torch.from_numpy(REF_PE_EI).to(DEV), u, v)
+    assert plan is not None and plan.cols == 6
+    m = REF_PE_MASK.reshape(3, 6)
+    y = plan.forward(engine.pack_masks(torch.from_numpy(m).to(DEV)))[:, 0].cpu().numpy()
+    ref = oracle.masked_edge_outputs(_spec(kind, dims, fc, model), x, REF_PE_EI, m, u, v)
+    np.testing.assert_allclose(y, ref, atol=1e-5)
 
 
 @pytest.mark.gpu

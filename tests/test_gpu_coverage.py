@@ -315,11 +315,14 @@ def test_wlm_fit_mc_exchange_failure_raises(monkeypatch):
     monkeypatch.setenv("XPG_MC_FAULT", "1")
     with pytest.raises(_lib.FitExchangeError):
         e.wlm_fit(*args)
-    status = torch.empty(1, dtype=torch.int32, device=DEV)
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
     e.wlm_fit(*args, check=False, status=status)  # deferred check: the word is set
     with pytest.raises(_lib.FitExchangeError):
         e.check_fit_status(status)
     monkeypatch.delenv("XPG_MC_FAULT")
+    e.wlm_fit(*args, check=False, status=status)  # a clean fit later: the word stays set (v13)
+    with pytest.raises(_lib.FitExchangeError):
+        e.check_fit_status(status)
     w, _, _, _, _ = e.wlm_fit(*args)
     ref, _, _ = oracle.train_wlm(m, B, y, k, w0, params)
     np.testing.assert_allclose(w.cpu().numpy(), ref, rtol=0, atol=1e-4)

@@ -336,6 +336,67 @@ def test_prepared_fit_equals_fit_from(S, R, B):
             assert torch.equal(pf[i].losses, ref[1]) and torch.equal(pf[i].best, ref[2])
 
 
+def test_pipelined_prepared_fits_equal_eager():
+    """bench.py's pipelined form: two PreparedFit buffer sets and a captured graph of two
+    consecutive steps, where step j fits set j & 1 on the capture stream while the next repeat's
+    masks -> forward -> KernelSHAP -> fit prologue fill the other set on a side stream.  Every
+    step of every replay equals the eager fit_from on the same seed bit for bit (w and losses),
+    and both sets' sticky status words stay clean over all replays."""
+    e = _eng()
+    exp, z, meta, ctx, plan = _plan_for(CASES[0])
+    S, R, B = plan.cols, 640, 64
+    W, steps = (S + 31) // 32, -(-R // B)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    w0 = torch.zeros((1, S), device=DEV)
+    seed_t = torch.full((1,), 700, dtype=torch.int64, device=DEV)
+    sets = [dict(bits=torch.empty((R, W), dtype=torch.int32, device=DEV),
+                 y=torch.empty((R, 1), dtype=torch.float32, device=DEV),
+                 k=torch.empty(R, dtype=torch.float64, device=DEV),
+                 cnt=torch.empty(R, dtype=torch.int32, device=DEV),
+                 fit=e.PreparedFit(1, R, S, B, params, DEV)) for _ in range(2)]
+    snaps = [(torch.empty((1, S), device=DEV), torch.empty((1, steps), dtype=torch.float64, device=DEV))
+             for _ in range(2)]
+    s1 = torch.cuda.Stream(device=DEV)
+
+    def produce(d):
+        e.sample_shapley_dev(seed_t, R, S, out=d["bits"])
+        seed_t.add_(1)
+        plan.forward(d["bits"], out=d["y"])
+        e.shap_kernel(d["bits"], S, out=d["k"], scratch=d["cnt"])
+        d["fit"].prepare(d["bits"], d["y"][:, 0], d["k"], w0)
+
+    def pipe_step(i, snap):
+        cur = torch.cuda.current_stream()
+        s1.wait_stream(cur)
+        d = sets[i]
+        w = d["fit"].fit(d["bits"], d["k"])
+        snap[0].copy_(w)
+        snap[1].copy_(d["fit"].losses)
+        with torch.cuda.stream(s1):
+            produce(sets[1 - i])
+        cur.wait_stream(s1)
+
+    produce(sets[0])  # prologue: seed 700
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for j in range(2):
+            pipe_step(j, snaps[j])
+    for rep in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        for j in range(2):
+            seed = 700 + 2 * rep + j
+            bits = e.sample_shapley(seed, R, S, DEV)
+            y = plan.forward(bits)[:, 0]
+            k = e.shap_kernel(bits, S)
+            ref = e.wlm_fit(bits.view(1, R, -1), S, B, y.view(1, R), k.view(1, R), w0, params)
+            assert torch.equal(snaps[j][0], ref[0]), (rep, j)
+            assert torch.equal(snaps[j][1], ref[1]), (rep, j)
+    for d in sets:
+        e.check_fit_status(d["fit"].status)
+
+
 def test_captured_repeat_equals_eager():
     """One repeat (device-seeded masks -> masked forward, KernelSHAP on a side stream ->
     fresh surrogate fit) captured in a HIP graph, as bench.py's headline replays it: every
