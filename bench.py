@@ -43,8 +43,8 @@ sys.path.insert(0, ROOT)
 METRIC = "perturbation-samples/sec (masked GNN fwd) per query node; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TF = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
-SECTIONS = ("headline", "c3", "c5", "gp", "c4", "comm", "queries")
-MULTI_GPU_SECTIONS = ("headline", "c3", "c5")
+SECTIONS = ("headline", "c3", "node_c3", "c5", "gp", "c4", "comm", "queries", "api")
+MULTI_GPU_SECTIONS = ("headline", "c3", "node_c3", "c5")
 
 
 def parse():
@@ -245,6 +245,8 @@ def roofline(alg_bytes, seconds, section=None, kernels=(), alg_per_kernel=None):
 
 # ----------------------------------------------------------------------------- c2 (headline)
 def build_c2(args, dev):
+    """configs[1]: the c2 graph, its 2-layer GCN and the 3-hop computational subgraph of the
+    query (Data.comp_graph with L + 1 hops, data.py:325-333)."""
     from bikg_graph_explainability_public_amd import pipeline
     from bikg_graph_explainability_public_amd.data import Data
     from bikg_graph_explainability_public_amd.nn import ConvStack
@@ -262,6 +264,54 @@ def build_c2(args, dev):
     return arch, sub_feat, sub_ei, q, plan
 
 
+def build_c3node(args, dev):
+    """configs[2] in the reference's node_prediction semantics (SURVEY.md §8d regime (i)): the
+    c3 graph (1M nodes / 10M edges, 128 feats), 2-layer SAGEConv(mean) 128 + Linear(128, 1) +
+    sigmoid, the 3-hop computational subgraph of the query."""
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.data import Data
+    x, ei, arch = c3_graph(dev)
+    arch = arch.to(dev)
+    data = Data(x.to(dev), ei.to(dev))
+    names = [str(i) for i in range(x.shape[0])]
+    sub_feat, sub_ei, _, sub_ind, _, _ = data.comp_graph(args.query, 2, "node", names)
+    q = int(sub_ind.reshape(-1)[0])
+    plan = pipeline.build_plan(arch, sub_feat, sub_ei, [q])
+    return arch, sub_feat, sub_ei, q, plan
+
+
+WORKLOADS = {
+    "c2": dict(build=build_c2, kind="gcn", samples=lambda a: a.interpret_samples,
+               text="c2 (BASELINE configs[1]): synthetic homogeneous 100k nodes / 1M edges, 64-dim "
+                    "feats, 2-layer GCN, interpret_samples=256, node_prediction (3-hop "
+                    "computational subgraph of node 7)"),
+    "c3node": dict(build=build_c3node, kind="sage", samples=lambda a: 512,
+                   text="c3 (BASELINE configs[2]) in node_prediction (SURVEY.md §8d regime (i)): "
+                        "synthetic homogeneous 1M nodes / 10M edges, 128-dim feats, 2-layer "
+                        "SAGEConv(mean) 128 + Linear(128, 1) + sigmoid, interpret_samples=512 "
+                        "(25,600 rows per repeat), 3-hop computational subgraph of node 7"),
+}
+
+
+def oracle_spec_of(arch, kind):
+    """The numpy oracle's model spec of a ConvStack (conv Linear weights + the dense head)."""
+    convs = []
+    for i in range(0, len(arch.conv), 2):
+        c = arch.conv[i]
+        if kind == "gcn":
+            prm = {"W": c.lin.weight.detach().cpu().numpy(), "b": c.bias.detach().cpu().numpy()}
+        else:
+            prm = {"Wl": c.lin_l.weight.detach().cpu().numpy(),
+                   "bl": c.lin_l.bias.detach().cpu().numpy(),
+                   "Wr": c.lin_r.weight.detach().cpu().numpy()}
+        convs.append({"kind": kind, "rels": [None], "act": "relu", "params": {None: prm}})
+    nfc = len(arch.fc) // 2
+    fc = [{"W": arch.fc[2 * i].weight.detach().cpu().numpy(),
+           "b": arch.fc[2 * i].bias.detach().cpu().numpy(),
+           "act": "sigmoid" if i == nfc - 1 else "relu"} for i in range(nfc)]
+    return {"convs": convs, "fc": fc}
+
+
 def wlm_bytes(rows, cols, batch):
     """Algorithmic bytes of one surrogate fit: the mask bits once, y + kernel, the Adam state
     (w, m, v read + written), one loss per step."""
@@ -272,12 +322,15 @@ def wlm_bytes(rows, cols, batch):
 WLM_KERNELS = ("k_wlm_prep", "k_wlm_fit_mc", "k_wlm_loss_best")
 
 
-def headline(args, dev, world, rank):
-    """The c2 repeat pipeline, sharded as Explainer.run shards it (module docstring)."""
+def headline(args, dev, world, rank, workload="c2"):
+    """The repeat pipeline of a node_prediction workload (c2: the headline; c3node: regime (i)
+    of configs[2]), sharded as Explainer.run shards it (module docstring)."""
     from bikg_graph_explainability_public_amd import engine, sharding
-    arch, sub_feat, sub_ei, q, plan = build_c2(args, dev)
+    wdef = WORKLOADS[workload]
+    arch, sub_feat, sub_ei, q, plan = wdef["build"](args, dev)
     S = plan.cols
-    R = args.interpret_samples * args.epochs
+    n_samples = wdef["samples"](args)
+    R = n_samples * args.epochs
     batch = R // args.epochs
     times = args.repeats * world
     n_rows = times * R
@@ -563,12 +616,12 @@ def headline(args, dev, world, rank):
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic",
-        "config": {"workload": "c2 (BASELINE configs[1]): synthetic homogeneous 100k nodes / 1M "
-                               "edges, 64-dim feats, 2-layer GCN, interpret_samples=256, "
-                               "node_prediction (3-hop computational subgraph of node 7)",
-                   "nodes": args.nodes, "edges": args.edges, "feat": args.feat,
+        "config": {"workload": wdef["text"],
+                   "nodes": args.nodes if workload == "c2" else 1_000_000,
+                   "edges": args.edges if workload == "c2" else 10_000_000,
+                   "feat": args.feat if workload == "c2" else 128,
                    "subgraph_nodes": S, "subgraph_edges": int(sub_ei.shape[1]),
-                   "interpret_samples": args.interpret_samples, "epochs": args.epochs,
+                   "interpret_samples": n_samples, "epochs": args.epochs,
                    "rows_per_repeat": R, "repeats_per_step": times,
                    "parallelism": f"dp{world}: one repeat per rank per step (its rows and its "
                                   "fit); per graph replay one async RCCL all-gather of the "
@@ -601,7 +654,8 @@ def headline(args, dev, world, rank):
                               "(i)); the HBM fraction is reported, not the bound"),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline_c2(args, arch, sub_feat, sub_ei, q)
+        line["cpu_baseline"] = cpu_baseline_subgraph(args, arch, wdef["kind"], sub_feat, sub_ei,
+                                                     q, n_samples)
     del plan
     return line
 
@@ -615,7 +669,7 @@ def _c2_cpu_worker(task):
         return oracle.masked_query_outputs(spec, x, {None: ei}, m, q, dtype=np.float32)
 
 
-def cpu_baseline_c2(args, arch, sub_feat, sub_ei, q):
+def cpu_baseline_subgraph(args, arch, kind, sub_feat, sub_ei, q, n_samples):
     """The numpy oracle (CPU restatement of the reference path) on the host cores: cpu_rows mask
     rows of the same workload, the union-graph forward split over worker processes, then
     KernelSHAP and the (sequential) surrogate fit."""
@@ -624,12 +678,7 @@ def cpu_baseline_c2(args, arch, sub_feat, sub_ei, q):
     rows = args.cpu_rows
     rng = np.random.default_rng(0)
     m = rng.random((rows, S)) < 0.5
-    spec = {"convs": [{"kind": "gcn", "rels": [None], "act": "relu",
-                       "params": {None: {"W": arch.conv[2 * i].lin.weight.detach().cpu().numpy(),
-                                         "b": arch.conv[2 * i].bias.detach().cpu().numpy()}}}
-                      for i in range(2)],
-            "fc": [{"W": arch.fc[0].weight.detach().cpu().numpy(),
-                    "b": arch.fc[0].bias.detach().cpu().numpy(), "act": "sigmoid"}]}
+    spec = oracle_spec_of(arch, kind)
     x, e = sub_feat.cpu().numpy(), sub_ei.cpu().numpy()
     procs = cpu_procs(args)
     chunks = [(spec, x, e, m[c], q) for c in np.array_split(np.arange(rows), procs * 4)]
@@ -638,7 +687,7 @@ def cpu_baseline_c2(args, arch, sub_feat, sub_ei, q):
         t0 = time.perf_counter()
         y = np.concatenate(pool.map(_c2_cpu_worker, chunks))
         k = oracle.shap_kernel(m)
-        oracle.train_wlm(m, args.interpret_samples, y, k, np.zeros(S, np.float32),
+        oracle.train_wlm(m, n_samples, y, k, np.zeros(S, np.float32),
                          {"lr": 0.01, "l1_lambda": 1e-4}, dtype=np.float32)
         dt = time.perf_counter() - t0
     model, ncpu = host_info()
@@ -646,7 +695,8 @@ def cpu_baseline_c2(args, arch, sub_feat, sub_ei, q):
             "host_cpu": model, "host_logical_cpus": ncpu, "host_cores": host_cores()[1],
             "sample": f"{rows} mask rows of the same workload (S={S}) through the numpy oracle: "
                       f"union-graph forward over {procs} worker processes (1 thread each), "
-                      f"KernelSHAP, surrogate fit; {dt:.1f} s"}
+                      f"KernelSHAP, surrogate fit ({n_samples} rows per Adam step); "
+                      f"{dt:.1f} s"}
 
 
 # ----------------------------------------------------------------------------- c3 (north star)
@@ -673,13 +723,38 @@ def full_graph_alg_bytes(n, e_kept_per_row, e, f_in, f_out, rows, layers=2):
     return layers * per_layer, per_layer
 
 
+def wide_kernel_bytes(n, e, f, rows, e_kept_rows, active_rows, gcn=False):
+    """Algorithmic HBM bytes of the implemented wide kernels over `rows` mask rows (32-row passes),
+    per kernel:
+      k_wide_l1s (layer 1): per pass the CSR (ptr, source positions, target positions, self
+        counts), the keep words of every in-edge and target, every in-edge's table row ONCE
+        (features are never masked: one read serves all 32 samples), the target's own table rows
+        (term + ROOT), the h1 rows of the samples that keep the target and one inactive row
+        (ctab) per target;
+      k_wide_last_ws (layer 2 + head): per pass the CSR (ptr, edge sources, source positions,
+        target positions, self counts), the keep words, per sample the h1 row of every kept
+        in-edge and the target's own row (h1 when the sample keeps it, else the shared ctab row,
+        one read per target), and the logits.
+    e_kept_rows / active_rows: per mask row, the kept-edge count and the active-node count."""
+    passes = -(-rows // 32)
+    fb = 4 * f
+    l1 = passes * (4 * (n + 1) + 4 * e + 8 * n + 4 * e + 4 * n + fb * e + 2 * fb * n + fb * n) + \
+        fb * float(np.sum(active_rows))
+    l2 = passes * (4 * (n + 1) + 8 * e + 12 * n + 4 * e + 4 * n + fb * n) + \
+        fb * float(np.sum(e_kept_rows)) + fb * float(np.sum(active_rows)) + 4 * rows * n
+    return {"k_wide_l1s": l1, "k_wide_last_ws": l2}
+
+
 C3_KERNELS = ("k_wide_bits", "k_wide_f0", "k_wide_degree", "k_wide_l1s", "k_wide_last_ws")
 
 
 def c3_section(args, dev, world, rank):
     """Regime (ii) on configs[2]: every node a target of the masked forward,
     c3_rows mask rows sharded over the ranks in 32-row passes (strong scaling), then the RCCL
-    all-gather of 64 query columns' logits of every row (what the surrogate fits consume)."""
+    all-gather of 64 query columns' logits of every row (what the surrogate fits consume).
+    Per-kernel device times come from HIP events the library records around each launch on its
+    stream (engine.profile_*), so every kernel's roofline fraction is its own bytes over its
+    own time; the line's roofline is the dominant kernel (layer 2)."""
     from bikg_graph_explainability_public_amd import engine, pipeline, sharding
     x, ei, arch = c3_graph(dev)
     N, E = x.shape[0], ei.shape[1]
@@ -697,6 +772,7 @@ def c3_section(args, dev, world, rank):
     reps = 3
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world)
+    engine.profile_enable(True)
     t0 = time.perf_counter()
     a.record(stream)
     for _ in range(reps):
@@ -707,17 +783,55 @@ def c3_section(args, dev, world, rank):
     barrier(world)
     wall = max_over_ranks((time.perf_counter() - t0) / reps, world, dev)
     fwd_ms = a.elapsed_time(b) / reps
+    kt = engine.profile_read()
+    engine.profile_enable(False)
     assert logits.shape == (total, qcols.numel())
-    # kept edges per row (both endpoints active), chunked, for the algorithmic byte count
-    kept = []
+    # per row: kept edges (both endpoints active) and active nodes, for the byte counts
+    kept, act = [], []
     for c0 in range(0, r1 - r0, 32):
         m = engine.unpack_masks(bits[c0:c0 + 32], N)
         kept.append((m[:, eid[0]] & m[:, eid[1]]).sum(1).double().cpu().numpy())
+        act.append(m.sum(1).double().cpu().numpy())
         del m
     kept = np.concatenate(kept) if kept else np.zeros(0)
-    alg, per_layer = full_graph_alg_bytes(N, kept, E, 128, 128, r1 - r0)
-    flops = (r1 - r0) * N * 2.0 * (2 * 128 * 128 + 128)  # layer-2 dense (l and r) + head
+    act = np.concatenate(act) if act else np.zeros(0)
     rows_rank = r1 - r0
+    alg_survey, per_layer = full_graph_alg_bytes(N, kept, E, 128, 128, rows_rank)
+    kb = wide_kernel_bytes(N, E, 128, rows_rank, kept, act)
+    npass = -(-rows_rank // 32)
+    slot = {"k_wide_l1s": "wide_l1", "k_wide_last_ws": "wide_l2"}
+    # counter bytes per 32-row pass from the section's PMC file (one op = one 512-row forward)
+    _, per_counter = pmc_chain("c3", set(C3_KERNELS))
+    kernels = {}
+    for k, sl in slot.items():
+        ms_tot, launches = kt[sl]
+        ms = ms_tot / max(1, launches)  # per launch = per 32-row pass
+        alg = kb[k] / npass
+        d = {"launch_ms": ms, "launches": launches, "alg_bytes_per_launch": alg,
+             "achieved_GBps": alg / (ms * 1e-3) / 1e9, "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        if per_counter is not None:
+            cb = per_counter[k] / 16.0  # the PMC ops are 512-row forwards = 16 passes
+            d.update(counter_bytes_per_launch=cb, counter_GBps=cb / (ms * 1e-3) / 1e9,
+                     frac_counter=cb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, counter_over_alg=cb / alg)
+        kernels[k] = d
+    dom = max(kernels, key=lambda k: kernels[k]["launch_ms"])
+    kd = kernels[dom]
+    other_ms = {k: kt[k][0] / max(1, kt[k][1]) for k in ("wide_bits", "wide_f0", "wide_degree")}
+    # the exact-f32 layer 2 (XPG_WIDE_B3=0) beside the default three-piece bf16 products: one pass
+    os.environ["XPG_WIDE_B3"] = "0"
+    try:
+        b32 = bits[:32]
+        y_b3 = plan.forward(b32)
+        engine.profile_enable(True)
+        y_ex = plan.forward(b32)
+        kt_ex = engine.profile_read()
+        engine.profile_enable(False)
+    finally:
+        os.environ.pop("XPG_WIDE_B3", None)
+    y_b3 = plan.forward(b32)
+    exact = {"layer2_ms": kt_ex["wide_l2"][0] / max(1, kt_ex["wide_l2"][1]),
+             "max_abs_diff_vs_bf16x3": float((y_ex - y_b3).abs().max())}
+    flops = rows_rank * N * 2.0 * (2 * 128 * 128 + 128)  # layer-2 dense (l and r) + head
     out = {
         "workload": "c3 (BASELINE configs[2]) full-graph masked forward (SURVEY.md §8d regime "
                     "(ii)): 1M nodes / 10M edges, 128 feats, 2-layer SAGEConv(mean) + "
@@ -725,17 +839,32 @@ def c3_section(args, dev, world, rank):
                     f"{total} mask rows sharded over {world} rank(s) in 32-row passes, then an "
                     "all-gather of 64 query columns of every row",
         "rows": total, "rows_per_rank": rows_rank, "ms": wall * 1e3,
-        "forward_ms_rank0": fwd_ms,
+        "forward_ms_rank0": fwd_ms, "pass_ms_rank0": fwd_ms / max(1, npass),
         "samples_per_s": total / wall,
         "samples_per_s_per_rank": rows_rank / (fwd_ms * 1e-3),
         "node_outputs_per_s": total * N / wall,
         "scaling": "strong",
-        "roofline": dict(roofline(alg, fwd_ms * 1e-3, "c3", C3_KERNELS),
-                         kernel="wide forward chain (" + ", ".join(C3_KERNELS) + ")",
-                         bytes_formula="SURVEY.md §8d B_alg per sample, E_kept measured per row",
-                         alg_bytes_per_layer=per_layer),
+        "kernels": kernels, "small_kernels_launch_ms": other_ms,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": kd["achieved_GBps"],
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kd["frac"],
+                     "bytes_per_launch": kd["alg_bytes_per_launch"],
+                     "traffic": kd.get("counter_bytes_per_launch"),
+                     "traffic_source": "profiles/pmc_c3.json" if per_counter else None,
+                     "frac_counter": kd.get("frac_counter"),
+                     "counter_over_alg": kd.get("counter_over_alg"),
+                     "time_source": "HIP events around each launch on its stream (xpg_profile_*)",
+                     "bytes_formula": "wide_kernel_bytes (implemented algorithm, per 32-row pass)"},
+        "survey_formula": {"alg_bytes": alg_survey, "alg_bytes_per_layer": per_layer,
+                           "achieved_GBps": alg_survey / (fwd_ms * 1e-3) / 1e9,
+                           "note": "SURVEY.md §8d B_alg per sample: counts layer 1's table-row "
+                                   "gather per sample (the kernel reads each row once per 32 "
+                                   "samples) and a 128-wide layer-2 output per node (the head "
+                                   "is fused: 4 B per node) — an upper bound on useful bytes, "
+                                   "not a fraction of peak"},
+        "layer2_exact_f32": exact,
         "mfma": {"tflops": flops / (fwd_ms * 1e-3) / 1e12, "peak_fp32_tflops": FP32_MFMA_PEAK_TF,
-                 "frac": flops / (fwd_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF},
+                 "note": "fp32-equivalent layer-2 + head flops over the whole chain time (the "
+                         "products run as three bf16 MFMAs): a rate, not MFMA-pipe utilisation"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_c3(args)
@@ -1178,6 +1307,72 @@ def graph_queries_section(args, dev, n=10_000, e=100_000, f=64, queries=8):
             "speedup": t_loop / t_shared}
 
 
+# ----------------------------------------------------------------------------- regime (i) c3, API
+def node_c3_section(args, dev, world, rank):
+    """configs[2] in node_prediction semantics (regime (i)): the headline's repeat pipeline on the
+    c3 graph's computational subgraph of node 7 (SAGE 128, interpret_samples=512), one repeat
+    per rank per step (weak scaling), with its own graph check and CPU baseline."""
+    line = headline(args, dev, world, rank, workload="c3node")
+    keep = ("value", "ms_per_step", "graph_check_max_abs_diff", "exchange_check_max_abs_diff",
+            "phases_ms", "cpu_baseline", "scaling")
+    out = {k: line[k] for k in keep if k in line}
+    out["samples_per_s"] = out.pop("value")
+    out["workload"] = line["config"]["workload"]
+    out["config"] = {k: v for k, v in line["config"].items() if k != "workload"}
+    out["roofline"] = dict(line["roofline"], traffic=None,
+                           note="latency-bound (cache-resident subgraph, regime (i)); HBM "
+                                "fraction reported, not the bound; no PMC pass for this section")
+    out["roofline"].pop("traffic_source", None)
+    for k in ("achieved_counter", "frac_counter", "counter_over_alg", "per_kernel_counter_bytes"):
+        out["roofline"].pop(k, None)
+    return out
+
+
+def explainer_section(args, dev):
+    """The public API end to end (Explainer(...).run(element, times), explainer.py:316-546):
+    host orchestration (hetero flattening, k-hop subgraph, plan, arch check), masks, forward,
+    KernelSHAP, surrogate fits, DataFrames — what a user calling run() gets, per phase
+    (Explainer.last_run["phases"]: host ms and device ms between phase marks).  c2 with the
+    device sampler (times=10) and the compat sampler (the reference's torch-CPU RNG order,
+    times=1); c3 node_prediction with the device sampler (times=10).  Second call of each timed
+    (the first one warms the code objects and allocator)."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    out = {}
+    g = torch.Generator().manual_seed(0)
+    feat = torch.randn((args.nodes, args.feat), generator=g)
+    ei = torch.randint(0, args.nodes, (2, args.edges), generator=g)
+    torch.manual_seed(0)
+    arch = ConvStack("gcn", [args.feat, 64, 64], [64, 1]).eval()
+    x3, ei3, arch3 = c3_graph(dev)
+    cases = [("c2_device_times10", feat, ei, arch, args.interpret_samples, "device", 10),
+             ("c2_compat_times1", feat, ei, arch, args.interpret_samples, "compat", 1),
+             ("c3node_device_times10", x3, ei3, arch3, 512, "device", 10)]
+    for name, f, e, a, ns, sampler, times in cases:
+        params = {"seed": 1, "interpret_samples": ns, "epochs": args.epochs, "optimizer": "adam",
+                  "lr": 0.01, "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": sampler}
+        names = [str(i) for i in range(f.shape[0])]
+        exp = Explainer(f.to(dev), e.to(dev), a, params, names)
+        exp.run(str(args.query), times)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        df, _ = exp.run(str(args.query), times)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ph = exp.last_run["phases"].times()
+        R = exp.last_run["repeats"][0]["rows"]
+        out[name] = {"samples_per_s": times * R / wall, "wall_ms": wall * 1e3, "rows": times * R,
+                     "times": times, "mask_sampler": sampler, "subgraph_nodes": exp.last_run["S"],
+                     "engine": bool(exp.last_run["engine"]), "phases": ph,
+                     "top_element": str(df.index[0])}
+        del exp
+        torch.cuda.empty_cache()
+    out["workload"] = ("Explainer(feat, edge_index, arch, params, names).run('7', times) end to "
+                       "end (node_prediction), inputs on the GPU; c2 = configs[1], c3node = "
+                       "configs[2] graph in node_prediction")
+    return out
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -1198,11 +1393,13 @@ def main():
     torch.cuda.empty_cache()
     regimes = {}
     runners = [("c3", "c3_full_graph", lambda: c3_section(args, dev, world, rank)),
+               ("node_c3", "node_c3", lambda: node_c3_section(args, dev, world, rank)),
                ("c5", "c5_hetero", lambda: c5_section(args, dev, world, rank)),
                ("gp", "graph_prediction_c3", lambda: graph_prediction_section(args, dev)),
                ("c4", "hetero_c4", lambda: hetero_c4_section(args, dev)),
                ("comm", "communities_c2", lambda: communities_section(args, dev)),
-               ("queries", "graph_queries", lambda: graph_queries_section(args, dev))]
+               ("queries", "graph_queries", lambda: graph_queries_section(args, dev)),
+               ("api", "explainer_api", lambda: explainer_section(args, dev))]
     for key, name, fn in runners:
         if key in want:
             t0 = time.perf_counter()

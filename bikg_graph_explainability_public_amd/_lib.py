@@ -81,6 +81,8 @@ _SIGS = {
                                ctypes.POINTER(ctypes.c_size_t)], c_i32),
     "xpg_masked_forward": ([ctypes.POINTER(ForwardPlanDesc), c_vp, c_i64, c_vp, c_vp,
                             ctypes.c_size_t, c_vp], c_i32),
+    "xpg_profile_enable": ([ctypes.c_int], c_i32),
+    "xpg_profile_read": ([c_vp, c_vp, c_i32], c_i32),
     "xpg_wlm_workspace": ([c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)], c_i32),
     "xpg_wlm_plan": ([c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)], c_i32),
     "xpg_wlm_fit": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, ctypes.POINTER(WlmParams), c_i64,

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/xpgnn.h"
 
@@ -1519,6 +1520,11 @@ struct WideArgs {
   int kind[XPG_MAX_TERMS], rel[XPG_MAX_TERMS];
   FusedHead H[kFusedMaxHead];
   float* out;  // layer 1: h1 [n_tgt][32][w_row] (node-major); last layer: y [rows][n_tgt]
+  // inactive-row table ctab [n1][w_row] (nullable): the layer-1 row of a target masked out in a
+  // sample does not depend on the sample (no kept in-edges: GCN keeps only the weight-1 self loop,
+  // MEAN is 0; the ROOT terms and bias are the node's own), so layer 1 stores h1 only for the
+  // samples that keep the target plus this one row, and layer 2 reads the row for the others
+  float* ctab;
 };
 
 constexpr int kWideCap = 256;  // staged in-edges per target (all terms, one per thread); more: in place
@@ -2221,7 +2227,7 @@ __device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8&
 // only consumes loads that were in flight during the previous interval; kept edges past the
 // first 4 of the first 16-edge chunk, and chunks past the first, are gathered in place.
 // Same summation order as the plain gather (bitwise the same A tile).
-template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false>
+template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false, int RPF = 4>
 __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(const WideArgs a) {
   constexpr int RIF = 8;
   // GW / TEAMS = 4 gather waves per target: a group owns samples g and g + 16; 8: sample g
@@ -2256,7 +2262,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     const float* base0 = a.src + (int64_t)(v0 ? s0 : 0) * a.w_row;
     const int32_t* smul = a.self_mult + (int64_t)ragg * a.n_tgt;
     const int kroot = 1 - kagg;  // host-checked: terms {MEAN, ROOT}
-    constexpr int RP = 4;        // prefetched kept rows per target (~2.5 kept per 16-edge chunk)
+    constexpr int RP = RPF;      // prefetched kept rows per target (~2.5 kept per 16-edge chunk)
     constexpr int RI = 4;        // rows per round of the in-place remainder
     __bf16* const Ab = reinterpret_cast<__bf16*>(wsm);
     // stage states: 1 = CSR range / node / prev position / self count, 2 = + this lane's edge,
@@ -2297,13 +2303,17 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       q4_tk = v0 && ((q3_mv >> s0) & 1u);
       uint32_t m0 = static_cast<uint32_t>(__ballot(q4_tk && ((q3_em >> s0) & 1u)) >> lb) & 0xFFFFu;
       q4_cnt = __popc(m0);
+      // the target's own row: its inactive-row table entry when the sample masks it out (ctab)
+      const float* p0r = a.ctab && !((q3_mv >> s0) & 1u) ? a.ctab + (int64_t)q3_tp * a.w_row + fo
+                                                          : base0 + (int64_t)q3_tp * a.rstride + fo;
 #pragma unroll
       for (int jj = 0; jj < RP; ++jj) {
         const int j = m0 ? __builtin_ctz(m0) : 0;
         q4_cv[jj] = m0 ? 1.f : 0.f;
         m0 &= m0 - 1u;
         const int srow = __shfl(q3_src, lb + j, 64);
-        const float* sp = base0 + (int64_t)(q4_cv[jj] != 0.f ? srow : q3_tp) * a.rstride + fo;
+        // an empty slot re-reads the own row (a written row: 0 x row stays finite)
+        const float* sp = q4_cv[jj] != 0.f ? base0 + (int64_t)srow * a.rstride + fo : p0r;
 #pragma unroll
         for (int x = 0; x < NFI / 4; ++x) {
           const float4 v = reinterpret_cast<const float4*>(sp)[x];
@@ -2314,7 +2324,6 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         }
       }
       q4_rest = m0;
-      const float* p0r = base0 + (int64_t)q3_tp * a.rstride + fo;
 #pragma unroll
       for (int x = 0; x < NFI / 4; ++x) {
         const float4 v = reinterpret_cast<const float4*>(p0r)[x];
@@ -2447,8 +2456,11 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         float* A = wsm + ((i & 1) * TEAMS + team) * abuf;
         float self0[NFI], self1[NFI];  // the target's own rows: the same for every term
         {
-          const float* p0r = base0 + (int64_t)tp * a.rstride + fo;
-          const float* p1r = base1 + (int64_t)tp * a.rstride + fo;
+          // ctab: a sample that masks the target out reads its inactive-row table entry
+          const float* p0r = a.ctab && !((mv >> s0) & 1u) ? a.ctab + (int64_t)tp * a.w_row + fo
+                                                           : base0 + (int64_t)tp * a.rstride + fo;
+          const float* p1r = a.ctab && !((mv >> s1) & 1u) ? a.ctab + (int64_t)tp * a.w_row + fo
+                                                           : base1 + (int64_t)tp * a.rstride + fo;
 #pragma unroll
           for (int q = 0; q < NFI; ++q) {
             self0[q] = p0r[q];
@@ -2918,6 +2930,11 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
         for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(static_cast<float>(sm), self[q], tot[s][q]) * inv;
       }
     }
+    // the row of a sample that masks the target out (ctab): no kept edge, GCN dt = 1 (the
+    // weight-1 self loop), MEAN 0 — the values tot[s] holds for such a sample, bit for bit
+    float cin[FPL];
+#pragma unroll
+    for (int q = 0; q < FPL; ++q) cin[q] = GCN ? fmaf(1.f, self[q], 0.f) : 0.f;
     for (int k = 1; k < a.n_terms; ++k) {  // ROOT terms (host-checked); term 1 prefetched
       float sk[FPL];
       if (k == 1 && a.n_terms == 2) {
@@ -2932,12 +2949,26 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
       for (int s = 0; s < 32; ++s)
 #pragma unroll
         for (int q = 0; q < FPL; ++q) tot[s][q] += sk[q];
+#pragma unroll
+      for (int q = 0; q < FPL; ++q) cin[q] += sk[q];
     }
     if (more) issueC();  // before the stores (see above)
+    // ctab: store only the samples that keep the target, plus the inactive row once
+    const uint32_t store_mask = a.ctab ? mv : 0xFFFFFFFFu;
+    if (a.ctab && mv != 0xFFFFFFFFu) {
+      float v[FPL];
+#pragma unroll
+      for (int q = 0; q < FPL; ++q)
+        v[q] = lane * FPL + q >= a.f_real ? 0.f
+               : a.act == XPG_ACT_RELU ? fmaxf(cin[q] + bv[q], 0.f) : act_apply(cin[q] + bv[q], a.act);
+      float* co = a.ctab + (int64_t)t * a.w_row + lane * FPL;
+#pragma unroll
+      for (int q = 0; q < FPL; ++q) co[q] = v[q];
+    }
     float* o = a.out + (int64_t)t * 32 * a.w_row + lane * FPL;
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
-      if (s < a.nr) {
+      if (s < a.nr && ((store_mask >> s) & 1u)) {
         float v[FPL];
         if (a.act == XPG_ACT_RELU) {  // one scalar branch, not a runtime switch per value
 #pragma unroll
@@ -3430,8 +3461,9 @@ __global__ __launch_bounds__(1024) void k_wlm_fit(
 //         (column vectors double-buffered: D(t) still reads Cb(t) while Cb(t+1) is stored)
 //   -- barrier 2 --
 constexpr uint32_t kMcSpinLimit = 1u << 21;
-constexpr int kMcMaxP = 16;
-constexpr int kMcMaxStage = 4;  // staged words per thread (rows and column vectors each)
+constexpr int kMcMaxP = 32;       // parts per fit (polled in rounds of kMcPollRound)
+constexpr int kMcPollRound = 16;
+constexpr int kMcMaxStage = 4;   // staged words per thread (rows and column vectors each; 8 spills)
 
 __device__ __forceinline__ void st64_sc1(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3704,29 +3736,36 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     if (wave < nrb) {
       float p = 0.f;
       if (prow) {
-        uint64_t gr[kMcMaxP];
+        // parts in rounds of kMcPollRound (all of a round's granule loads in flight, then the
+        // bounded spins), summed in part order 0..P-1 either way
+        for (int q0 = 0; q0 < P; q0 += kMcPollRound) {
+          uint64_t gr[kMcPollRound];
 #pragma unroll
-        for (int q = 0; q < kMcMaxP; ++q)
-          gr[q] = q < P && q != part ? ld64_sc1(xs + q * (int64_t)batch + j) : (static_cast<uint64_t>(tag) << 32);
+          for (int qq = 0; qq < kMcPollRound; ++qq) {
+            const int q = q0 + qq;
+            gr[qq] = q < P && q != part ? ld64_sc1(xs + q * (int64_t)batch + j) : (static_cast<uint64_t>(tag) << 32);
+          }
 #pragma unroll
-        for (int q = 0; q < kMcMaxP; ++q) {
-          if (q < P) {
-            uint32_t n = 0;
-            while (static_cast<uint32_t>(gr[q] >> 32) != tag) {
-              __builtin_amdgcn_s_sleep(1);
-              gr[q] = ld64_sc1(xs + q * (int64_t)batch + j);
-              ++n;
-              // bounded: a partner that never publishes (grid not co-resident, or a partner
-              // that already left after an error) ends the fit with the error word set, which
-              // xpg_wlm_fit hands to the caller's status word
-              if (n > spin_limit || ((n & 63u) == 0 &&
-                                     __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                abort_s = 1;
-                break;
+          for (int qq = 0; qq < kMcPollRound; ++qq) {
+            const int q = q0 + qq;
+            if (q < P) {
+              uint32_t n = 0;
+              while (static_cast<uint32_t>(gr[qq] >> 32) != tag) {
+                __builtin_amdgcn_s_sleep(1);
+                gr[qq] = ld64_sc1(xs + q * (int64_t)batch + j);
+                ++n;
+                // bounded: a partner that never publishes (grid not co-resident, or a partner
+                // that already left after an error) ends the fit with the error word set, which
+                // xpg_wlm_fit hands to the caller's status word
+                if (n > spin_limit || ((n & 63u) == 0 &&
+                                       __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                  __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  abort_s = 1;
+                  break;
+                }
               }
+              p += q == part ? pown : __uint_as_float(static_cast<uint32_t>(gr[qq]));
             }
-            p += q == part ? pown : __uint_as_float(static_cast<uint32_t>(gr[q]));
           }
         }
       }
@@ -4377,9 +4416,30 @@ int device_cus() {
   return cus;
 }
 
+// Optional per-kernel timing (xpg_profile_enable / xpg_profile_read): a pair of hipEvents on the
+// launch stream around each profiled launch, read back (and released) by xpg_profile_read.  Off
+// by default; never enable it around a graph capture.
+bool g_prof_on = false;
+struct ProfRec {
+  hipEvent_t a, b;
+  int slot;
+};
+std::vector<ProfRec> g_prof;
+void prof_begin(hipStream_t st, int slot) {
+  if (!g_prof_on || g_prof.size() >= 65536) return;
+  ProfRec r{nullptr, nullptr, slot};
+  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return;
+  (void)hipEventRecord(r.a, st);
+  g_prof.push_back(r);
+}
+void prof_end(hipStream_t st, int slot) {
+  if (!g_prof_on || g_prof.empty() || g_prof.back().slot != slot) return;
+  (void)hipEventRecord(g_prof.back().b, st);
+}
+
 // Wide (full-graph) forward: 2-layer plans with large frontiers (returns 1 when it does not apply).
 struct WideWs {
-  size_t mT, mT0, kin, h1, total;
+  size_t mT, mT0, kin, h1, ct, total;
   int nfi, a_ld, h_ld, o_h0, o_h1, o_e, kw;
   int o_hw[kFusedMaxHead];
   size_t lds;
@@ -4445,6 +4505,8 @@ int wide_layout(const xpg_forward_plan* p, WideWs* W) {
   off += align_up(W->gcn ? sizeof(float) * 32 * (size_t)p->n_rel * p->n0 : 0);
   W->h1 = off;
   off += align_up(sizeof(float) * 32 * (size_t)l1.n_tgt * f1);
+  W->ct = off;  // inactive-row table of layer 1 (WideArgs::ctab)
+  off += align_up(sizeof(float) * (size_t)l1.n_tgt * f1);
   W->total = off;
   return 0;
 }
@@ -4587,14 +4649,27 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const bool pipe = b3 && teams == 1 && gw == 8 && a2.n_terms == 2 && a2.agg1 >= 0 &&
                     a2.kind[a2.agg1] == XPG_TERM_MEAN && a2.kind[1 - a2.agg1] == XPG_TERM_ROOT &&
                     !(ppe && std::strcmp(ppe, "0") == 0);
+  // prefetched kept rows per group and target of the pipelined gather (XPG_WIDE_RP: 4, 6 or 8;
+  // default 6: a target's in-edges keep ~2.5 rows per sample, and one of its 32 samples past the
+  // prefetched ones costs the whole interval a dependent load round)
+  const char* rpe = getenv("XPG_WIDE_RP");
+  const int rpf = rpe ? atoi(rpe) : 6;
   if (ws2) {
-    if (pipe) k2 = k_wide_last_ws<8, 32, 8, true, 1, true>;
+    if (pipe) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8>
+                 : rpf == 6 ? k_wide_last_ws<8, 32, 8, true, 1, true, 6>
+                            : k_wide_last_ws<8, 32, 8, true, 1, true, 4>;
     else if (teams == 2) k2 = b3 ? k_wide_last_ws<8, 32, 8, true, 2> : k_wide_last_ws<8, 32, 8, false, 2>;
     else if (gw == 8) k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 8, true> : kw32 ? k_wide_last_ws<8, 32, 8> : k_wide_last_ws<8, 0, 8>)
                                      : (kw32 ? k_wide_last_ws<4, 32, 8> : k_wide_last_ws<4, 0, 8>);
     else k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 4, true> : kw32 ? k_wide_last_ws<8, 32, 4> : k_wide_last_ws<8, 0, 4>)
                         : (kw32 ? k_wide_last_ws<4, 32, 4> : k_wide_last_ws<4, 0, 4>);
   }
+  // inactive-row table (XPG_WIDE_CT=0: h1 holds every sample's row) for the default pair
+  // k_wide_l1s -> k_wide_last_ws; the other kernels read / write h1 only
+  const char* cte = getenv("XPG_WIDE_CT");
+  const bool l1s_k = k1 == k_wide_l1s<1, true> || k1 == k_wide_l1s<1, false> || k1 == k_wide_l1s<2, true> ||
+                     k1 == k_wide_l1s<2, false> || k1 == k_wide_l1s<4, true> || k1 == k_wide_l1s<4, false>;
+  if (ws2 && l1s_k && !(cte && std::strcmp(cte, "0") == 0)) a1.ctab = a2.ctab = reinterpret_cast<float*>(ws + W.ct);
   const size_t lds2 = ws2 ? lds_ws : W.lds;
   const char* gwe0 = getenv("XPG_WIDE_GW");
   const int thr2 = ws2 ? 64 * ((gwe0 && atoi(gwe0) == 4 ? 4 : 8) + 4) : 256;
@@ -4616,26 +4691,36 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const unsigned g2 = static_cast<unsigned>(std::min<int64_t>(l2.n_tgt, per_cu2 * (int64_t)cus));
   for (int64_t r0 = 0; r0 < rows; r0 += kWideS) {
     const int nr = static_cast<int>(std::min<int64_t>(kWideS, rows - r0));
+    prof_begin(st, XPG_PROF_WIDE_BITS);
     hipLaunchKernelGGL(k_wide_bits, dim3(static_cast<unsigned>(cdiv(words, 256))), dim3(256), 0, st, bits, r0, nr,
                        words, p->cols, mT);
     XPG_LAUNCHED();
+    prof_end(st, XPG_PROF_WIDE_BITS);
+    prof_begin(st, XPG_PROF_WIDE_F0);
     hipLaunchKernelGGL(k_wide_f0, dim3(static_cast<unsigned>(cdiv(p->n0, 256))), dim3(256), 0, st, mT, p->f0_node,
                        p->n0, mT0);
     XPG_LAUNCHED();
+    prof_end(st, XPG_PROF_WIDE_F0);
     if (W.gcn) {
       const int64_t n = (int64_t)p->n_rel * p->n0 * 32;
+      prof_begin(st, XPG_PROF_WIDE_DEGREE);
       hipLaunchKernelGGL(k_wide_degree, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, st, mT, mT0, p->n0,
                          p->n_rel, p->deg_ptr, p->deg_src, kinT);
       XPG_LAUNCHED();
+      prof_end(st, XPG_PROF_WIDE_DEGREE);
     }
     a1.nr = nr;
     a1.row0 = r0;
+    prof_begin(st, XPG_PROF_WIDE_L1);
     hipLaunchKernelGGL(k1, dim3(g1), dim3(thr1), lds1, st, a1);
     XPG_LAUNCHED();
+    prof_end(st, XPG_PROF_WIDE_L1);
     a2.nr = nr;
     a2.row0 = r0;
+    prof_begin(st, XPG_PROF_WIDE_L2);
     hipLaunchKernelGGL(k2, dim3(g2), dim3(thr2), lds2, st, a2);
     XPG_LAUNCHED();
+    prof_end(st, XPG_PROF_WIDE_L2);
   }
   return XPG_OK;
 }
@@ -4935,6 +5020,38 @@ int xpg_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t ld
   return launch_dense(A, M, lda, W, ldw, k_pad, bias, n_real, n_pad, act, C, ldc, S(stream));
 }
 
+int xpg_profile_enable(int on) {
+  for (ProfRec& r : g_prof) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  g_prof.clear();
+  g_prof_on = on != 0;
+  return XPG_OK;
+}
+
+int xpg_profile_read(double* ms, int64_t* launches, int32_t n_slots) {
+  XPG_REQ(ms != nullptr && launches != nullptr && n_slots > 0, "profile_read: bad arguments");
+  for (int i = 0; i < n_slots; ++i) {
+    ms[i] = 0.0;
+    launches[i] = 0;
+  }
+  int rc = XPG_OK;
+  for (ProfRec& r : g_prof) {
+    float t = 0.f;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&t, r.a, r.b) != hipSuccess) rc = XPG_EHIP;
+    if (r.slot >= 0 && r.slot < n_slots) {
+      ms[r.slot] += t;
+      ++launches[r.slot];
+    }
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  g_prof.clear();
+  if (rc) return fail(rc, "profile_read: event timing failed");
+  return XPG_OK;
+}
+
 int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* bytes) {
   WsLayout L;
   int rc = layout_ws(plan, rows, &L);
@@ -5177,7 +5294,9 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
     const char* xe = getenv("XPG_MC_XCD");
     L->xcd = !(xe && std::strcmp(xe, "0") == 0);
     const char* pe = getenv("XPG_MC_P");  // tuning override of the parts per fit
-    int P = std::min(kMcMaxP, std::max(2, pe ? atoi(pe) : static_cast<int>(cdiv(words, 3))));
+    // up to 16 parts by default (the exchange is one poll round); more only when the staging
+    // budget asks for them (the loop below, at most kMcMaxP)
+    int P = std::min(pe ? kMcMaxP : kMcPollRound, std::max(2, pe ? atoi(pe) : static_cast<int>(cdiv(words, 3))));
     // stagers: the waves past the B / poll waves when batch <= 512 (k_wlm_fit_mc's split_stage)
     const int64_t nrb = cdiv(batch, 64), ns = nrb <= 8 ? 1024 - 64 * nrb : 1024;
     // the staged rows / column vectors must fit kMcMaxStage words per stager: more parts if not

@@ -223,6 +223,26 @@ def dense(A: torch.Tensor, W: torch.Tensor, bias, act=None, n_real=None) -> torc
     return C[:, :N]
 
 
+# ----------------------------------------------------------------------------- kernel timing
+PROF_SLOTS = ("wide_bits", "wide_f0", "wide_degree", "wide_l1", "wide_l2")
+
+
+def profile_enable(on=True):
+    """Per-kernel HIP-event timing of the wide forward path (xpg_profile_enable): measurement
+    only, never around a graph capture."""
+    _lib.check(_lib.load().xpg_profile_enable(1 if on else 0))
+
+
+def profile_read():
+    """{slot: (device ms summed over launches, launches)} since profile_enable (waits for the
+    recorded events; xpg_profile_read)."""
+    n = len(PROF_SLOTS)
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_int64 * n)()
+    _lib.check(_lib.load().xpg_profile_read(ms, cnt, n))
+    return {k: (ms[i], cnt[i]) for i, k in enumerate(PROF_SLOTS)}
+
+
 # ----------------------------------------------------------------------------- forward plan
 def plan_arrays(S, rel_np, queries, L, rel_eid=None):
     """Receptive-field frontiers and CSR arrays (numpy; see include/xpgnn.h).

@@ -11,6 +11,7 @@ Repeats draw masks and the surrogate's initial weights from torch's CPU generato
 reference's order (compat sampler), so results match the reference CPU path for the same seed.
 """
 import random
+import time
 import warnings
 
 import numpy as np
@@ -22,6 +23,34 @@ from .masks import Mask, dataloader_seed_draw
 from .model import Model
 from .pathways import Pathways
 from .wlm import LinearRegression
+
+
+class PhaseClock:
+    """Phase boundaries of one run: a host timestamp and a CUDA event on the current stream at
+    each mark (no synchronisation); `times()` synchronises once and returns, per phase, the
+    host wall milliseconds and the device milliseconds between its two events."""
+
+    def __init__(self):
+        self.marks = []
+
+    def mark(self, name):
+        ev = None
+        if torch.cuda.is_available():
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        self.marks.append((name, time.perf_counter(), ev))
+
+    def times(self):
+        if len(self.marks) < 2:
+            return {}
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        out = {}
+        for (name, t0, e0), (_, t1, e1) in zip(self.marks, self.marks[1:]):
+            out[name] = {"host_ms": (t1 - t0) * 1e3,
+                         "device_ms": e0.elapsed_time(e1) if e0 is not None else None}
+        out["total_host_ms"] = (self.marks[-1][1] - self.marks[0][1]) * 1e3
+        return out
 
 
 def set_seed(seed=100):
@@ -201,6 +230,8 @@ class Explainer:
             raise _lib.NativeLibraryError("Explainer.run needs an MI355X (HIP) device; "
                                           "there is no CPU fallback")
         _lib.load()
+        clock = PhaseClock()
+        clock.mark("setup")
         device = torch.device("cuda", torch.cuda.current_device())
         if times == 1:
             set_seed(self.params["seed"])
@@ -208,7 +239,9 @@ class Explainer:
         # masks / sampler seeds / initial weights (checked by checksum below)
         sharding.sync_rng(self.group)
         self.arch = self.arch.to(device).eval()
+        clock.mark("prepare")
         c = self.prepare(element, device)
+        clock.mark("plan")
         sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
 
@@ -218,6 +251,7 @@ class Explainer:
         else:
             plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, [sub_ind], *geo)
             verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo)
+        clock.mark("verify")
         if plan is not None and self.params.get("verify_arch", True):
             ok, err = verify()
             if not ok:
@@ -225,6 +259,7 @@ class Explainer:
                               " using the generic torch path")
                 plan = None
 
+        clock.mark("sample")
         sampler = self.params.get("mask_sampler", "compat")
         _, epochs = Mask.assertions_mask_generator(self.params)
         # draw every repeat's masks and initial surrogate weights first, in the reference's
@@ -281,6 +316,7 @@ class Explainer:
                 return torch.empty(0, dtype=torch.float64, device=device)
             return engine.shap_kernel(flat[s:e], S)
         kern = None
+        clock.mark("forward_shap")
         if plan is not None:
             # KernelSHAP needs only the mask bits: its kernels run on a side stream beside the
             # masked forward (sharding.gather_map_beside)
@@ -313,6 +349,7 @@ class Explainer:
             kern = sharding.gather_map(times * R, kernel_rows, g).reshape(times, R)
 
         fits = {}
+        clock.mark("fit")
 
         def fit(t0, t1):
             if t1 == t0:
@@ -331,14 +368,17 @@ class Explainer:
         diag = [{"losses": losses[i], "best_epoch": best[i], "rows": R, "batch": batch,
                  "y": y[i], "bits": bits[i], "kernel": kern[i], "w0": w0_list[i]}
                 for i in range(times)]
+        clock.mark("output")
         mean, std = self.weight_stacking(config_vals)
         config_val_df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
         pathway_df = None
         if c["has_pathways"]:
             pathway_df = Pathways(c["sub_pw"], c["sub_pw_names"]).aggregate(mean,
                                                                             c["sub_pw_inds"])
+        clock.mark("end")
         self.last_run = {"engine": plan is not None, "repeats": diag, "S": S,
-                         "sub_ind": sub_ind, "plan": plan, "weights": config_vals}
+                         "sub_ind": sub_ind, "plan": plan, "weights": config_vals,
+                         "phases": clock}
         return config_val_df, pathway_df
 
     def run_queries(self, elements, times=1):

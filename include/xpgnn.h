@@ -4,8 +4,9 @@
  * Every entry point is `extern "C"`, takes plain device pointers + sizes + a HIP stream
  * (`xpg_stream_t`, NULL = legacy default stream) and returns an int status (XPG_OK = 0);
  * `xpg_last_error()` returns a thread-local message for the last failure.  No entry point
- * allocates, frees or synchronises: device memory (inputs, outputs, workspaces) is owned by the
- * caller (PyTorch tensors in the Python host), so every call can be captured in a hipGraph.
+ * allocates, frees or synchronises (the xpg_profile_* measurement hooks aside): device memory
+ * (inputs, outputs, workspaces) is owned by the caller (PyTorch tensors in the Python host), so
+ * every call can be captured in a hipGraph.
  *
  * Mask bit layout ("row bits"): uint32 [rows][words], words = ceil(cols / 32); element c of
  * row r is bit (c & 31) of word r*words + (c >> 5).  Bits past `cols` in the last word are 0.
@@ -191,6 +192,16 @@ int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* by
  * y[r] = the decoded score of the target pair (dot_a, dot_b). */
 int xpg_masked_forward(const xpg_forward_plan* plan, const uint32_t* bits, int64_t rows,
                        float* y, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
+
+/* Optional per-kernel timing of xpg_masked_forward's wide (full-graph) path (v13): with profiling
+ * on, every launch of a profiled kernel is bracketed by two hipEvents on its stream;
+ * xpg_profile_read waits for them and returns, per slot, the summed device milliseconds and the
+ * launch count, then releases them.  xpg_profile_enable (0 / 1) also drops unread records.  For
+ * measurement only: never enable it around a graph capture.  Slots: */
+enum xpg_prof_slot { XPG_PROF_WIDE_BITS = 0, XPG_PROF_WIDE_F0 = 1, XPG_PROF_WIDE_DEGREE = 2,
+                     XPG_PROF_WIDE_L1 = 3, XPG_PROF_WIDE_L2 = 4, XPG_PROF_SLOTS = 5 };
+int xpg_profile_enable(int on);
+int xpg_profile_read(double* ms, int64_t* launches, int32_t n_slots);
 
 /* ---------------------------------------------------------------- weighted linear surrogate */
 typedef struct xpg_wlm_params {

@@ -66,6 +66,14 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_PIPE", "0")
     else:
         monkeypatch.delenv("XPG_WIDE_PIPE", raising=False)
+    if path == "wide-noct":  # h1 holds every sample's row (no inactive-row table)
+        monkeypatch.setenv("XPG_WIDE_CT", "0")
+    else:
+        monkeypatch.delenv("XPG_WIDE_CT", raising=False)
+    if path == "wide-rp4":  # 4 prefetched kept rows per gather group (default 6)
+        monkeypatch.setenv("XPG_WIDE_RP", "4")
+    else:
+        monkeypatch.delenv("XPG_WIDE_RP", raising=False)
 
 
 def _spec(kind, dims, fc, arch):
@@ -102,7 +110,7 @@ def _masks(R, S, seed):
 
 # ------------------------------------------------------------------ hubs, all targets
 @pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "wide-teams",
-                                  "wide-nopipe", "unfused"])
+                                  "wide-nopipe", "wide-noct", "wide-rp4", "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1])])

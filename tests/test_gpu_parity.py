@@ -30,7 +30,7 @@ def _eng():
 
 
 @pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather", "wide-exact",
-                        "wide-teams", "wide-nopipe"])
+                        "wide-teams", "wide-nopipe", "wide-noct", "wide-rp4"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
@@ -40,7 +40,8 @@ def fwd_path(request, monkeypatch):
     gather layer-1 kernel instead of the default one-wave-per-target k_wide_l1s; "wide-exact" =
     layer 2 on the exact fp32 MFMA instead of the three-piece bf16 products; "wide-teams" = the
     layer-2 kernel with two gather teams, two targets in flight per interval; "wide-nopipe" = the
-    B3 layer-2 kernel without the cross-target pipelined gather)."""
+    B3 layer-2 kernel without the cross-target pipelined gather; "wide-noct" = h1 holds every
+    sample's row (no inactive-row table); "wide-rp4" = 4 prefetched kept rows per group (default 6))."""
     monkeypatch.setenv("XPG_FORWARD", request.param.split("-")[0])
     if request.param in ("wide-mfma", "wide-gather"):
         monkeypatch.setenv("XPG_WIDE_L1", request.param.split("-")[1])
@@ -50,6 +51,10 @@ def fwd_path(request, monkeypatch):
         monkeypatch.setenv("XPG_WIDE_TEAMS", "2")
     if request.param == "wide-nopipe":
         monkeypatch.setenv("XPG_WIDE_PIPE", "0")
+    if request.param == "wide-noct":
+        monkeypatch.setenv("XPG_WIDE_CT", "0")
+    if request.param == "wide-rp4":
+        monkeypatch.setenv("XPG_WIDE_RP", "4")
     return request.param
 
 

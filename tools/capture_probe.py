@@ -10,13 +10,18 @@ one line per variant and stops at the first child killed by a signal:
   alloc_side  an allocation on a side stream that was never forked from the capture stream
   unjoined    side stream forked from the capture stream, work on it, NOT joined before the
               capture ends
+  timing_ev   a timing-enabled CUDA event recorded inside the capture
+  ext_wait    a side stream waits on an event recorded BEFORE the capture, then joins
+  replay_in   another graph replayed while this one is being captured
+  graph_gc    a graph object dropped (freed) while another is being captured
 
     python tools/capture_probe.py [variant ...]
 """
 import subprocess
 import sys
 
-VARIANTS = ("joined", "sync", "alloc_side", "unjoined")
+VARIANTS = ("joined", "sync", "alloc_side", "unjoined", "timing_ev", "ext_wait", "replay_in",
+            "graph_gc")
 
 
 def child(variant):
@@ -24,12 +29,32 @@ def child(variant):
     dev = torch.device("cuda", 0)
     x = torch.ones(1 << 20, device=dev)
     side = torch.cuda.Stream(device=dev)
+    pre = torch.cuda.Event()
+    pre.record()
+    other = torch.cuda.CUDAGraph()
+    if variant in ("replay_in", "graph_gc"):
+        with torch.cuda.graph(other):
+            x.mul_(1.0)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         cur = torch.cuda.current_stream()
         y = x * 2
-        if variant == "sync":
+        if variant == "timing_ev":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+        elif variant == "ext_wait":
+            side.wait_event(pre)
+            with torch.cuda.stream(side):
+                z = x + 1
+            cur.wait_stream(side)
+        elif variant == "replay_in":
+            other.replay()
+        elif variant == "graph_gc":
+            del other
+            import gc
+            gc.collect()
+        elif variant == "sync":
             float(y.sum().item())
         elif variant == "alloc_side":
             with torch.cuda.stream(side):  # never waited on the capture stream
