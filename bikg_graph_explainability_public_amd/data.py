@@ -45,6 +45,12 @@ def k_hop_subgraph(node_idx, num_hops, edge_index, num_nodes=None):
     return subset, remap[edge_index[:, emask]], inv[:1], emask
 
 
+def take_names(names, idx):
+    """np.array(names, dtype=str)[idx].tolist() without converting every name: the selected
+    names as numpy's str conversion gives them."""
+    return np.array([names[int(i)] for i in idx], dtype=str).tolist() if len(idx) else []
+
+
 def pad_feat_tensors(feat_tensors):
     """data.py:825-878 — zero-pad feature widths to the maximum; returns (padded tensors,
     padding per type, start pointer per type)."""
@@ -140,13 +146,12 @@ class Data:
             sub_ei = torch.tensor([[int(sub_ind)], [int(sub_ind)]], dtype=torch.long,
                                   device=self.edge_index.device)
         sub_feat = self.feat[subset]
-        names_arr = np.array(names, dtype=str)
         sub_nt = node_types[subset] if node_types is not None else None
         sub_et = edge_types[torch.where(emask)[0]] if edge_types is not None else None
-        if "node" in problem or "graph" in problem:
-            sub_names = names_arr[subset.cpu().numpy()].tolist()
-        else:
-            sub_names = names_arr[torch.where(emask)[0].cpu().numpy()].tolist()
+        pos = subset if "node" in problem or "graph" in problem else torch.where(emask)[0]
+        # the reference indexes np.array(names, dtype=str) (data.py:341-356); only the subgraph's
+        # names are converted here, not every name of the graph (1M of them at c3)
+        sub_names = take_names(names, pos.cpu().numpy())
         return sub_feat, sub_ei, sub_names, sub_ind, sub_nt, sub_et
 
     def edge_comp_graph(self, ind, n_hops, names):
@@ -171,7 +176,7 @@ class Data:
         keep = node[ei[0]] & node[ei[1]]
         pos = torch.nonzero(keep).reshape(-1)
         sub_ind = int(torch.nonzero(pos == int(ind)).reshape(-1)[0])
-        sub_names = np.array(names, dtype=str)[pos.cpu().numpy()].tolist()
+        sub_names = take_names(names, pos.cpu().numpy())
         return (self.feat[subset], remap[ei[:, keep]], sub_names, sub_ind,
                 (int(remap[u]), int(remap[v])))
 

@@ -127,11 +127,17 @@ class Explainer:
 
     @staticmethod
     def extract_index(element, names=None):
-        """explainer.py:191-226."""
+        """explainer.py:191-226: the first position whose name (as numpy's str) equals element.
+        String elements look up a name -> first position index built once per names list (the
+        reference converts the whole list to a numpy str array on every call: ~50 ms at 1M)."""
         if names is None:
             assert isinstance(element, (int, float)), \
                 "No element names have been given and the node name given is not numeric"
             return int(element)
+        if isinstance(element, str):
+            members, idx = _name_index(names)
+            assert element in members, "Element name '{}' is not present in the graph".format(element)
+            return idx[element]
         assert element in names, "Element name '{}' is not present in the graph".format(element)
         return int(np.where(np.array(names, dtype=str) == element)[0][0])
 
@@ -497,6 +503,27 @@ class Explainer:
                          "bits": bits, "y": y, "kernel": kern, "w0": w0_all.reshape(Q, times, S),
                          "weights": fitted, "plan": plan}
         return out
+
+
+_NAME_INDEX = {}
+
+
+def _name_index(names):
+    """(set(names), {str(name): first position}) of a names list — `element in names` and the
+    reference's np.where(np.array(names, dtype=str) == element)[0][0] as lookups — cached by
+    identity and length (a list edited in place to the same length keeps a stale index)."""
+    key = (id(names), len(names))
+    hit = _NAME_INDEX.get(key)
+    if hit is not None and hit[0] is names:
+        return hit[1], hit[2]
+    strs = np.array(names, dtype=str).tolist() if len(names) else []
+    idx = {}
+    for i, n in enumerate(strs):
+        idx.setdefault(n, i)
+    if len(_NAME_INDEX) > 8:
+        _NAME_INDEX.clear()
+    _NAME_INDEX[key] = (names, set(names), idx)
+    return _NAME_INDEX[key][1], idx
 
 
 def _to_device(x, device):

@@ -571,6 +571,30 @@ def test_wlm_fit_vs_oracle_large(R, S, B, wlm_path, monkeypatch):
     np.testing.assert_allclose(losses.cpu().numpy(), rl, rtol=1e-5)
 
 
+def test_wlm_fit_midsize_many_fits_multi_vs_oracle():
+    """S = 10,000 columns, 8 fits in one launch (the graph_queries shape, batch 256): the
+    multi-workgroup fit takes it with more than 16 parts per fit (two poll rounds; it went to
+    the single-workgroup fit before), every fit vs the fp64 oracle."""
+    e = _eng()
+    F, R, S, B = 8, 2560, 10_000, 256
+    kind, parts = e.wlm_plan(F, R, S, B)
+    assert kind == "multi" and parts > 16, (kind, parts)
+    rng = np.random.default_rng(8)
+    m = rng.random((F, R, S)) < 0.5
+    y = rng.random((F, R)).astype(np.float32)
+    k = np.stack([oracle.shap_kernel(m[f]) for f in range(F)])
+    w0 = ((rng.random((F, S)) - 0.5) * 0.02).astype(np.float32)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    bits = torch.stack([e.pack_masks(torch.as_tensor(m[f]).to(DEV)) for f in range(F)])
+    w, losses, best, _, _ = e.wlm_fit(bits, S, B, torch.as_tensor(y), torch.as_tensor(k),
+                                      torch.as_tensor(w0), params)
+    for f in range(F):
+        ref, rl, rb = oracle.train_wlm(m[f], B, y[f], k[f], w0[f], params)
+        np.testing.assert_allclose(w[f].cpu().numpy(), ref, rtol=0, atol=1e-4)
+        np.testing.assert_allclose(losses[f].cpu().numpy(), rl, rtol=1e-5)
+        assert int(best[f]) == rb
+
+
 def test_wlm_fit_many_columns_vs_oracle():
     """S = 40,000 columns (> 16384: the grid fit), two independent fits in one call."""
     e = _eng()
