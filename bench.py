@@ -1009,7 +1009,7 @@ def c5_section(args, dev, world, rank):
         y = torch.stack([pipeline.multi_type_targets(y[i], empty[i], batch, q, S, q4=True)
                          for i in range(f0, f1)]) if f1 > f0 else y[:0]
         mk(4)
-        st = torch.empty(1, dtype=torch.int32, device=dev)
+        st = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky status word: starts at 0
         if f1 > f0:
             w, _, _, _, _ = engine.wlm_fit(bits[f0:f1], S, batch, y, k[f0:f1], w0[f0:f1], fit,
                                            check=False, status=st)

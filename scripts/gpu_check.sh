@@ -33,6 +33,10 @@ for step in "$@"; do
            run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/calib_fetch -o run -- ./tools/fetch_calib && \
            run calib_write 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/calib_write -o run -- ./tools/fetch_calib ;;
     fwdprobe) XPG_LIB=tools/libxpgnn_stamps.so run fwdprobe 300 python tools/fwd_probe.py ;;
+    # k_wlm_fit_mc mode A/B (tools/wlm_probe stamps, c2 fit shape): 0 base, 1 late stage,
+    # 2 split poll, 3 both; alternating rounds on one box
+    modes) for r in 1 2; do for md in 0 1 2 3; do XPG_MC_MODE=$md run probe_mode${md}_r$r 120 ./tools/wlm_probe 1193 12800 256; done; done ;;
+    gw2) run gw2 300 ./tools/gw2_probe ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;
     profall) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profall -o run -- python3 bench.py --no-cpu-baseline ;;
