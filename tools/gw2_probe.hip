@@ -193,6 +193,158 @@ __global__ __launch_bounds__(WAVES * 64) void grad_kernel(const uint32_t* __rest
   }
 }
 
+// v2 candidates: the lookups of two rows (16 table reads) issued before any of them is summed,
+// the rows of the batch split over gridDim.y workgroups (balanced grids), 16 lookups per round
+template <int WAVES, int MODE>
+__global__ __launch_bounds__(WAVES * 64) void p2_kernel(const uint32_t* __restrict__ bits, int64_t rows, int64_t cols,
+                                                        int64_t words, int batch, int64_t t,
+                                                        const float* __restrict__ wg, float* __restrict__ p_part) {
+  __shared__ float T[8 * 16 * kGwWords];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  p_part += (int64_t)blockIdx.x * batch;
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const int rper = (((B + gridDim.y - 1) / gridDim.y) + 31) & ~31;  // rows of this workgroup's share
+  const int rlo = blockIdx.y * rper, rhi = min(B, rlo + rper);
+  const int64_t w0 = (int64_t)blockIdx.x * kGwWords;
+  const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
+  const uint32_t lmask = lane < nw ? ~0u : 0u;
+  const uint32_t wd = static_cast<uint32_t>(w0 + (lane < nw ? lane : 0));
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  uint32_t x[32];
+  int rb = rlo + wv * 32;
+  if (rb < rhi) gw_load32<MODE>(bits, words, r0 + rb, min(32, rhi - rb), wd, x);
+  for (int task = tid; task < 8 * kGwWords; task += WAVES * 64) {
+    const int j = task & (kGwWords - 1), q = task >> 6;
+    const int64_t c = (w0 + j) * 32 + 4 * q;
+    float a[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) a[b] = c + b < cols ? wg[c + b] : 0.f;
+    float* Tq = T + q * 16 * kGwWords + j;
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      Tq[v * kGwWords] = ((v & 1) ? a[0] : 0.f) + ((v & 2) ? a[1] : 0.f) + ((v & 4) ? a[2] : 0.f) +
+                         ((v & 8) ? a[3] : 0.f);
+  }
+  __syncthreads();
+  const float* Tl = T + lane;
+#pragma unroll 1
+  for (; rb < rhi; rb += WAVES * 32) {
+    const int nr = min(32, rhi - rb);
+    uint32_t xn[32];
+    const int rbn = rb + WAVES * 32;
+    if (rbn < rhi) gw_load32<MODE>(bits, words, r0 + rbn, min(32, rhi - rbn), wd, xn);
+    float c[32];
+#pragma unroll
+    for (int i = 0; i < 32; i += 2) {
+      const uint32_t x0 = i < nr ? (x[i] & lmask) : 0u, x1 = i + 1 < nr ? (x[i + 1] & lmask) : 0u;
+      float a0[8], a1[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        a0[q] = Tl[(q * 16 + ((x0 >> (4 * q)) & 15u)) * kGwWords];
+        a1[q] = Tl[(q * 16 + ((x1 >> (4 * q)) & 15u)) * kGwWords];
+      }
+      c[i] = ((a0[0] + a0[1]) + (a0[2] + a0[3])) + ((a0[4] + a0[5]) + (a0[6] + a0[7]));
+      c[i + 1] = ((a1[0] + a1[1]) + (a1[2] + a1[3])) + ((a1[4] + a1[5]) + (a1[6] + a1[7]));
+    }
+    const float tot = wave_transpose_reduce32(c, lane);
+    const int i = (lane >> 1) & 31;
+    if (!(lane & 1) && i < nr) p_part[rb + i] = tot;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) x[k] = xn[k];
+  }
+}
+
+template <int WAVES, int MODE>
+__global__ __launch_bounds__(WAVES * 64) void grad2_kernel(const uint32_t* __restrict__ bits, int64_t rows,
+                                                           int64_t cols, int64_t words, int batch, int64_t t,
+                                                           const float* __restrict__ g, float* __restrict__ wg,
+                                                           float* __restrict__ mg, float* __restrict__ vg) {
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const int ngrp = ((B + 31) / 32) * 8;
+  const int64_t w0 = (int64_t)blockIdx.x * kGwWords;
+  const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
+  const uint32_t lmask = lane < nw ? ~0u : 0u;
+  const uint32_t wd = static_cast<uint32_t>(w0 + (lane < nw ? lane : 0));
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  uint32_t x[32];
+  if (wv * 32 < B) gw_load32<MODE>(bits, words, r0 + wv * 32, min(32, B - wv * 32), wd, x);
+  // the chunk's Adam state, in flight during the whole sweep (8 columns per thread at 4 waves)
+  constexpr int CPT = 32 * kGwWords / (WAVES * 64);
+  float wr[CPT], mr[CPT], vr[CPT];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int64_t c = w0 * 32 + tid + k * WAVES * 64;
+    wr[k] = c < cols ? wg[c] : 0.f;
+    mr[k] = c < cols ? mg[c] : 0.f;
+    vr[k] = c < cols ? vg[c] : 0.f;
+  }
+  const int gp = ngrp | 1;
+  float* G = gsm;
+  float* part = gsm + ((16 * gp + 3) & ~3);  // [WAVES][32 bit][65]
+  for (int grp = tid; grp < ngrp; grp += WAVES * 64) {
+    float a[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) a[b] = 4 * grp + b < B ? g[4 * grp + b] : 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      G[v * gp + grp] = ((v & 1) ? a[0] : 0.f) + ((v & 2) ? a[1] : 0.f) + ((v & 4) ? a[2] : 0.f) +
+                        ((v & 8) ? a[3] : 0.f);
+  }
+  __syncthreads();
+  float acc[32];
+#pragma unroll
+  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+#pragma unroll 1
+  for (int rb = wv; rb * 32 < B; rb += WAVES) {
+    const int nr = min(32, B - rb * 32);
+    uint32_t xn[32];
+    const int rbn = rb + WAVES;
+    if (rbn * 32 < B) gw_load32<MODE>(bits, words, r0 + rbn * 32, min(32, B - rbn * 32), wd, xn);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) x[i] = i < nr ? (x[i] & lmask) : 0u;
+    transpose32(x);
+    const float* Gb = G + rb * 8;
+#pragma unroll
+    for (int b = 0; b < 32; b += 2) {
+      float a0[8], a1[8];
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        a0[n] = Gb[((x[b] >> (4 * n)) & 15u) * gp + n];
+        a1[n] = Gb[((x[b + 1] >> (4 * n)) & 15u) * gp + n];
+      }
+      acc[b] += ((a0[0] + a0[1]) + (a0[2] + a0[3])) + ((a0[4] + a0[5]) + (a0[6] + a0[7]));
+      acc[b + 1] += ((a1[0] + a1[1]) + (a1[2] + a1[3])) + ((a1[4] + a1[5]) + (a1[6] + a1[7]));
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) x[k] = xn[k];
+  }
+  // every wave's column partials to LDS at once, one barrier, summed in wave order
+#pragma unroll
+  for (int b = 0; b < 32; ++b) part[(wave * 32 + b) * 65 + lane] = acc[b];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int e = tid + k * WAVES * 64;
+    const int64_t c = w0 * 32 + e;
+    float gsum = 0.f;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) gsum += part[(w * 32 + (e & 31)) * 65 + (e >> 5)];
+    if (c < cols) {
+      float w = wr[k], m = mr[k], v = vr[k];
+      m = fmaf(0.1f, gsum - m, m);
+      v = fmaf(0.001f, gsum * gsum, v * 0.999f);
+      w = w - 0.01f * (m / (sqrtf(v) + 1e-8f));
+      wg[c] = w;
+      mg[c] = m;
+      vg[c] = v;
+    }
+  }
+}
+
 // pure streaming read of the step's rows: lane = VEC words of a 64 * VEC word chunk (blockIdx.x),
 // the rows of the batch split over gridDim.y workgroups and their WAVES waves in blocks of RIF
 // rows (all RIF loads of a block in flight); one xor-sum per lane written
@@ -286,6 +438,21 @@ int main() {
   });
   P(8, 0) P(8, 1) P(8, 2) P(4, 0) P(16, 0)
   G(4, 0) G(4, 1) G(4, 2) G(8, 0) G(16, 0)
+#define P2(WV, MD, SPLIT)                                                                                  \
+  timeit("p2<" #WV "," #MD "> x" #SPLIT, [&](int t) {                                                      \
+    hipLaunchKernelGGL((p2_kernel<WV, MD>), dim3(n_wg, SPLIT), dim3(WV * 64), 0, 0, bits, rows, cols, words, B, \
+                       t, w, p_part);                                                                      \
+  });
+  P2(8, 0, 1) P2(8, 2, 1) P2(4, 0, 2) P2(4, 2, 2) P2(8, 0, 2) P2(4, 0, 4)
+  const size_t lds_g2 = sizeof(float) * (size_t)(((16 * (((B + 31) / 32) * 8 | 1) + 3) & ~3) + 8 * 32 * 65);
+#define G2(WV, MD)                                                                                         \
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&grad2_kernel<WV, MD>),                                \
+                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_g2));               \
+  timeit("grad2<" #WV "," #MD ">", [&](int t) {                                                            \
+    hipLaunchKernelGGL((grad2_kernel<WV, MD>), dim3(n_wg), dim3(WV * 64), lds_g2, 0, bits, rows, cols, words, \
+                       B, t, g, w, m, v);                                                                  \
+  });
+  G2(4, 0) G2(4, 2) G2(8, 0) G2(8, 2)
 #define SK(VEC, WV, RIF, SPLIT)                                                                            \
   timeit("stream<" #VEC "," #WV "," #RIF "> x" #SPLIT, [&](int t) {                                        \
     hipLaunchKernelGGL((stream_kernel<VEC, WV, RIF>), dim3((words + 64 * VEC - 1) / (64 * VEC), SPLIT),     \
