@@ -37,6 +37,9 @@ for step in "$@"; do
     # 2 split poll, 3 both; alternating rounds on one box
     modes) for r in 1 2; do for md in 0 1 2 3; do XPG_MC_MODE=$md run probe_mode${md}_r$r 120 ./tools/wlm_probe 1193 12800 256; done; done ;;
     gw2) run gw2 300 ./tools/gw2_probe ;;
+    wsprof) run wsprof 700 bash scripts/ws_prof.sh ;;
+    apiprof) run apiprof 300 python -u tools/api_profile.py ;;
+    wsprof2) run wsprof2 600 bash scripts/ws_prof2.sh ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;
     profall) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profall -o run -- python3 bench.py --no-cpu-baseline ;;

@@ -1,0 +1,55 @@
+"""Diagnostic (not part of the product): where the host time of Explainer.run goes (cProfile of
+one warm run on the c2 workload, device sampler, times=10), top functions by cumulative time.
+
+    python tools/api_profile.py [--times 10] [--sampler device]
+"""
+import argparse
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bikg_graph_explainability_public_amd.explainer import Explainer  # noqa: E402
+from bikg_graph_explainability_public_amd.nn import ConvStack  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--times", type=int, default=10)
+    p.add_argument("--sampler", default="device")
+    p.add_argument("--top", type=int, default=45)
+    args = p.parse_args()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(0)
+    n, e, f = 100_000, 1_000_000, 64
+    feat = torch.randn((n, f), generator=g)
+    ei = torch.randint(0, n, (2, e), generator=g)
+    torch.manual_seed(0)
+    arch = ConvStack("gcn", [f, 64, 64], [64, 1]).eval()
+    params = {"seed": 1, "interpret_samples": 256, "epochs": 50, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": args.sampler}
+    exp = Explainer(feat.to(dev), ei.to(dev), arch, params, [str(i) for i in range(n)])
+    exp.run("8", args.times)
+    torch.cuda.synchronize()
+    for q in ("9", "10"):
+        t0 = time.perf_counter()
+        exp.run(q, args.times)
+        torch.cuda.synchronize()
+        print(f"run({q}, {args.times}): {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+    pr = cProfile.Profile()
+    pr.enable()
+    exp.run("7", args.times)
+    torch.cuda.synchronize()
+    pr.disable()
+    ph = exp.last_run["phases"].times()
+    print({k: round(v["host_ms"], 3) for k, v in ph.items() if isinstance(v, dict)}, flush=True)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(args.top)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+
+
+if __name__ == "__main__":
+    main()
