@@ -2227,7 +2227,19 @@ __device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8&
 // only consumes loads that were in flight during the previous interval; kept edges past the
 // first 4 of the first 16-edge chunk, and chunks past the first, are gathered in place.
 // Same summation order as the plain gather (bitwise the same A tile).
-template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false, int RPF = 4>
+// IDX (with PIPE): the target's index work is done ONCE per workgroup instead of by each of the 32
+// gather groups (they all read the same CSR range, edge list and keep words, which hold every
+// sample's bit): MFMA wave 0 -- idle most of each interval -- runs that chain two targets ahead
+// (CSR range -> first kIxEdges in-edges -> keep words, software-pipelined one stage per
+// interval) and leaves per target the edges' source rows and 32-sample kept masks
+// (source keep word & target keep word) in an LDS ring of three lists.  A gather group then
+// reads its kept edges from the list (ballots over the mask bits), so its own chain per target
+// is LDS -> kept rows.  In-degrees past kIxEdges keep the in-place path.  Same summation order as
+// the plain gather: bitwise the same A tile.
+constexpr int kIxEdges = 32;                 // listed in-edges per target (32-bit kept masks)
+constexpr int kIxInts = 2 * kIxEdges + 8;    // src[32] | km[32] | b0 b1 tp sm mv + pad
+template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false, int RPF = 4,
+          bool IDX = false>
 __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(const WideArgs a) {
   constexpr int RIF = 8;
   // GW / TEAMS = 4 gather waves per target: a group owns samples g and g + 16; 8: sample g
@@ -2246,6 +2258,8 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   // every A read waited for its LDS latency right before its MFMA)
   constexpr bool WL = B3 && TEAMS == 1;
   __bf16* WLs = reinterpret_cast<__bf16*>(H0 + 2 * TEAMS * a.f_out_pad);
+  // IDX: three in-edge lists [kIxInts] after the weight lo pieces (16-B aligned)
+  int* IX = reinterpret_cast<int*>(WLs + (WL ? (int64_t)a.K * a.f_out_pad : 0));
   const int ntgt_wg = a.n_tgt > (int)blockIdx.x ? (a.n_tgt - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int nint = (ntgt_wg + TEAMS - 1) / TEAMS;  // intervals (one LDS barrier each)
   const int kagg = a.agg1;
@@ -2254,7 +2268,237 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   if constexpr (PIPE) {
     static_assert(!TWO && TEAMS == 1 && B3, "pipelined gather: one sample per group, one team, B3 tiles");
   }
-  if (PIPE && wave < GW) {
+  static_assert(!IDX || PIPE, "shared index lists: pipelined gather only");
+  const int32_t* smul_all = a.self_mult + (int64_t)ragg * a.n_tgt;
+  // ---- IDX index chain (MFMA wave 0, lane = listed edge): stage A = CSR range / target fields,
+  // B = the first kIxEdges edges' sources, C = keep words -> the LDS list of the target
+  int qa_b0 = 0, qa_b1 = 0, qa_tf0 = 0, qa_tp = 0, qa_sm = 0;
+  int qb_b0 = 0, qb_b1 = 0, qb_tf0 = 0, qb_tp = 0, qb_sm = 0, qb_src = 0, qb_u0 = 0;
+  int qc_b0 = 0, qc_b1 = 0, qc_tp = 0, qc_sm = 0, qc_src = 0;
+  uint32_t qc_mv = 0u, qc_em = 0u;
+  auto stA = [&](int k) {
+    if (k >= ntgt_wg) return;
+    const int t = blockIdx.x + k * gridDim.x;
+    qa_b0 = aptr[t];
+    qa_b1 = aptr[t + 1];
+    qa_tf0 = a.tgt_f0[t];
+    qa_tp = a.tgt_prev[t];
+    qa_sm = smul_all[t];
+  };
+  auto stB = [&](int k) {
+    if (k >= ntgt_wg) return;
+    qb_b0 = qa_b0; qb_b1 = qa_b1; qb_tf0 = qa_tf0; qb_tp = qa_tp; qb_sm = qa_sm;
+    const int e = qa_b0 + lane;
+    qb_src = e < qa_b1 && lane < kIxEdges ? a.agg_src[e] : 0;
+    qb_u0 = e < qa_b1 && lane < kIxEdges ? a.agg_f0[e] : 0;
+  };
+  auto stC_load = [&](int k) {
+    if (k >= ntgt_wg) return;
+    qc_b0 = qb_b0; qc_b1 = qb_b1; qc_tp = qb_tp; qc_sm = qb_sm; qc_src = qb_src;
+    qc_mv = a.mT0[qb_tf0];
+    qc_em = qb_b0 + lane < qb_b1 && lane < kIxEdges ? a.mT0[qb_u0] : 0u;
+  };
+  auto stC_store = [&](int k) {
+    if (k >= ntgt_wg) return;
+    int* ix = IX + (k % 3) * kIxInts;
+    if (lane < kIxEdges) {
+      ix[lane] = qc_src;
+      ix[kIxEdges + lane] = static_cast<int>(qc_em & qc_mv);
+    }
+    if (lane == 0) {
+      ix[2 * kIxEdges] = qc_b0;
+      ix[2 * kIxEdges + 1] = qc_b1;
+      ix[2 * kIxEdges + 2] = qc_tp;
+      ix[2 * kIxEdges + 3] = qc_sm;
+      ix[2 * kIxEdges + 4] = static_cast<int>(qc_mv);
+    }
+  };
+  const bool ixw = IDX && wave == GW && !(a.dbg & 32);  // the index wave (MFMA wave 0)
+  if constexpr (IDX) {
+    // prologue: the lists of targets 0 and 1, the chain state of targets 2 (B) and 3 (A)
+    if (ixw) {
+      stA(0); stB(0); stC_load(0); stC_store(0);
+      stA(1); stB(1); stC_load(1); stC_store(1);
+      stA(2); stB(2); stA(3);
+    }
+    lds_barrier();
+  }
+  if (PIPE && IDX && wave < GW) {
+    // ------------------------------------------------------------------ gather role, shared lists
+    const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
+    const int s0 = g;
+    const bool v0 = s0 < a.nr;
+    const float* base0 = a.src + (int64_t)(v0 ? s0 : 0) * a.w_row;
+    constexpr int64_t RS = 32 * 16 * NFI;  // h1 row stride (node-major: 32 samples x w_row floats)
+    const int kroot = 1 - kagg;            // host-checked: terms {MEAN, ROOT}
+    constexpr int RP = RPF;
+    constexpr int RI = 4;
+    __bf16* const Ab = reinterpret_cast<__bf16*>(wsm);
+    uint32_t p_rest = 0u;
+    int p_cnt = 0, p_sm = 0, p_b0 = 0, p_b1 = 0, p_fill = 0;
+    bool p_tk = false;
+    float p_cv[RP], p_row[RP][NFI], p_self[NFI];
+#pragma unroll
+    for (int jj = 0; jj < RP; ++jj)
+#pragma unroll
+      for (int x = 0; x < NFI; ++x) p_row[jj][x] = 0.f;  // slots keep finite values: 0 x stale row = 0
+    // the next target's kept edges from its list (wave-uniform k: the ballots see every lane),
+    // its first RP kept rows (slot jj loaded only by the groups with a jj-th kept edge, and only
+    // while some group of the wave has one) and its own row in flight
+    auto prefetch = [&](int k) {
+      if (k >= ntgt_wg) return;
+      const int* ix = IX + (k % 3) * kIxInts;
+      const int b0 = ix[2 * kIxEdges], b1 = ix[2 * kIxEdges + 1], tp = ix[2 * kIxEdges + 2];
+      const uint32_t mv = static_cast<uint32_t>(ix[2 * kIxEdges + 4]);
+      const bool tk = v0 && ((mv >> s0) & 1u);
+      const int ne = min(b1 - b0, kIxEdges);
+      uint32_t M = 0u;
+#pragma unroll
+      for (int c = 0; c < kIxEdges / 16; ++c) {
+        if (16 * c < ne) {  // workgroup-uniform
+          const uint32_t km = 16 * c + gl < ne ? static_cast<uint32_t>(ix[kIxEdges + 16 * c + gl]) : 0u;
+          M |= (static_cast<uint32_t>(__ballot(tk && ((km >> s0) & 1u)) >> lb) & 0xFFFFu) << (16 * c);
+        }
+      }
+      p_cnt = __popc(M);
+      p_tk = tk;
+      p_sm = ix[2 * kIxEdges + 3];
+      p_b0 = b0;
+      p_b1 = b1;
+      const float* p0r = a.ctab && !((mv >> s0) & 1u) ? a.ctab + (int64_t)tp * a.w_row + fo
+                                                       : base0 + (int64_t)tp * RS + fo;
+      int fill = 0;
+#pragma unroll
+      for (int jj = 0; jj < RP; ++jj) {
+        p_cv[jj] = M ? 1.f : 0.f;
+        if (__ballot(M != 0u) != 0ull) {  // wave-uniform: some group has a jj-th kept edge
+          fill = jj + 1;
+          if (M) {
+            const int j = __builtin_ctz(M);
+            const float* sp = base0 + (int64_t)ix[j] * RS + fo;
+#pragma unroll
+            for (int x = 0; x < NFI / 4; ++x) {
+              const float4 v = reinterpret_cast<const float4*>(sp)[x];
+              p_row[jj][4 * x] = v.x;
+              p_row[jj][4 * x + 1] = v.y;
+              p_row[jj][4 * x + 2] = v.z;
+              p_row[jj][4 * x + 3] = v.w;
+            }
+          }
+        }
+        M &= M - 1u;
+      }
+      p_fill = fill;
+      p_rest = M;
+#pragma unroll
+      for (int x = 0; x < NFI / 4; ++x) {
+        const float4 v = reinterpret_cast<const float4*>(p0r)[x];
+        p_self[4 * x] = v.x;
+        p_self[4 * x + 1] = v.y;
+        p_self[4 * x + 2] = v.z;
+        p_self[4 * x + 3] = v.w;
+      }
+    };
+    const bool run = !(a.dbg & 32);  // dbg 32 (diagnostics): no gathers
+    if (run) prefetch(0);
+    for (int i = 0; i <= nint + 1; ++i) {
+      if (run && i < ntgt_wg) {
+        float acc[NFI];
+#pragma unroll
+        for (int x = 0; x < NFI; ++x) acc[x] = 0.f;
+#pragma unroll
+        for (int q = 0; q < RP; ++q)
+          if (q < p_fill) {  // wave-uniform
+#pragma unroll
+            for (int x = 0; x < NFI; ++x) acc[x] = fmaf(p_cv[q], p_row[q][x], acc[x]);
+          }
+        // listed kept edges past the prefetched ones, in place (ctz order), RI rows per round
+        const int* ix = IX + (i % 3) * kIxInts;
+        uint32_t m = p_rest;
+        while (m) {  // group-uniform
+          float rr[RI][NFI];
+          float cv[RI];
+#pragma unroll
+          for (int q = 0; q < RI; ++q) {
+            const int j = m ? __builtin_ctz(m) : 0;
+            cv[q] = m ? 1.f : 0.f;
+            m &= m - 1u;
+            const float* sp = base0 + (int64_t)ix[j] * RS + fo;
+#pragma unroll
+            for (int x = 0; x < NFI / 4; ++x) {
+              const float4 v = reinterpret_cast<const float4*>(sp)[x];
+              rr[q][4 * x] = v.x;
+              rr[q][4 * x + 1] = v.y;
+              rr[q][4 * x + 2] = v.z;
+              rr[q][4 * x + 3] = v.w;
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < RI; ++q)
+#pragma unroll
+            for (int x = 0; x < NFI; ++x) acc[x] = fmaf(cv[q], rr[q][x], acc[x]);
+        }
+        int cnt = p_cnt;
+        // in-edges past the list (in-degree > kIxEdges): straight from the CSR, in place
+        for (int c0 = p_b0 + kIxEdges; c0 < p_b1; c0 += 16) {
+          const int e = c0 + gl;
+          const int esrc = e < p_b1 ? a.agg_src[e] : 0;
+          const int eu0 = e < p_b1 ? a.agg_f0[e] : 0;
+          const uint32_t em = e < p_b1 ? a.mT0[eu0] : 0u;
+          uint32_t mm = static_cast<uint32_t>(__ballot(p_tk && ((em >> s0) & 1u)) >> lb) & 0xFFFFu;
+          cnt += __popc(mm);
+          while (mm) {
+            float rr[RI][NFI];
+            float cv[RI];
+#pragma unroll
+            for (int q = 0; q < RI; ++q) {
+              const int j = mm ? __builtin_ctz(mm) : 0;
+              cv[q] = mm ? 1.f : 0.f;
+              mm &= mm - 1u;
+              const int srow = __shfl(esrc, lb + j, 64);
+              const float* sp = base0 + (int64_t)srow * RS + fo;
+#pragma unroll
+              for (int x = 0; x < NFI / 4; ++x) {
+                const float4 v = reinterpret_cast<const float4*>(sp)[x];
+                rr[q][4 * x] = v.x;
+                rr[q][4 * x + 1] = v.y;
+                rr[q][4 * x + 2] = v.z;
+                rr[q][4 * x + 3] = v.w;
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < RI; ++q)
+#pragma unroll
+              for (int x = 0; x < NFI; ++x) acc[x] = fmaf(cv[q], rr[q][x], acc[x]);
+          }
+        }
+        const float inv = p_tk ? 1.f / static_cast<float>(max(cnt + p_sm, 1)) : 0.f;
+        float self[NFI];
+#pragma unroll
+        for (int x = 0; x < NFI; ++x) {
+          self[x] = p_self[x];
+          acc[x] = fmaf(static_cast<float>(p_sm), self[x], acc[x]) * inv;
+        }
+        __bf16* A = Ab + (i & 1) * 2 * abuf;  // abuf floats = 2 abuf bf16
+        bf16x8 hi, lo;
+#pragma unroll
+        for (int x = 0; x < NFI; ++x) {
+          acc[x] = v0 ? acc[x] : 0.f;
+          self[x] = v0 ? self[x] : 0.f;
+        }
+        split_bf16x8(acc, hi, lo);
+        const int ea = s0 * aph + kagg * a.w_row + fo;
+        *reinterpret_cast<bf16x8*>(A + ea) = hi;
+        *reinterpret_cast<bf16x8*>(A + 32 * aph + ea) = lo;
+        split_bf16x8(self, hi, lo);
+        const int er = s0 * aph + kroot * a.w_row + fo;
+        *reinterpret_cast<bf16x8*>(A + er) = hi;
+        *reinterpret_cast<bf16x8*>(A + 32 * aph + er) = lo;
+        prefetch(i + 1);  // list of target i + 1: written at interval i - 1 (or the prologue)
+      }
+      lds_barrier();
+    }
+  } else if (PIPE && wave < GW) {
     // ------------------------------------------------------------------ pipelined gather role
     const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
     const int s0 = g;
@@ -2632,6 +2876,11 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       }
     }
     for (int i = 0; i <= nint + 1; ++i) {
+      if (ixw) {  // index chain: keep words of i + 2 (stored below), edges of i + 3, range of i + 4
+        stC_load(i + 2);
+        stB(i + 3);
+        stA(i + 4);
+      }
 #pragma unroll
       for (int j = 0; j < TEAMS; ++j) {  // targets of interval i - 2: y[s] = act(sum over blocks + b)
         const int idx = TEAMS * (i - 2) + j;
@@ -2756,6 +3005,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         }
       }
       }
+      if (ixw) stC_store(i + 2);  // the list of target i + 2 (read from interval i + 1 on)
       lds_barrier();
     }
   }
@@ -4650,14 +4900,21 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
                     a2.kind[a2.agg1] == XPG_TERM_MEAN && a2.kind[1 - a2.agg1] == XPG_TERM_ROOT &&
                     !(ppe && std::strcmp(ppe, "0") == 0);
   // prefetched kept rows per group and target of the pipelined gather (XPG_WIDE_RP: 4, 6 or 8;
-  // default 6: a target's in-edges keep ~2.5 rows per sample, and one of its 32 samples past the
-  // prefetched ones costs the whole interval a dependent load round)
+  // a target's in-edges keep ~2.5 rows per sample, and one of its 32 samples past the prefetched
+  // ones costs the whole interval a dependent load round)
+  // shared in-edge lists (IDX: the target's index chain once per workgroup, XPG_WIDE_IDX=0 off)
+  const char* ixe = getenv("XPG_WIDE_IDX");
+  const bool idx = pipe && !(ixe && std::strcmp(ixe, "0") == 0);
+  // (IDX: empty slots cost no loads, default 8: the c3 pass 17.3 -> 17.0 ms over 6)
   const char* rpe = getenv("XPG_WIDE_RP");
-  const int rpf = rpe ? atoi(rpe) : 6;
+  const int rpf = rpe ? atoi(rpe) : idx ? 8 : 6;
   if (ws2) {
-    if (pipe) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8>
-                 : rpf == 6 ? k_wide_last_ws<8, 32, 8, true, 1, true, 6>
-                            : k_wide_last_ws<8, 32, 8, true, 1, true, 4>;
+    if (pipe && idx) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8, true>
+                        : rpf == 6 ? k_wide_last_ws<8, 32, 8, true, 1, true, 6, true>
+                                   : k_wide_last_ws<8, 32, 8, true, 1, true, 4, true>;
+    else if (pipe) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8>
+                      : rpf == 6 ? k_wide_last_ws<8, 32, 8, true, 1, true, 6>
+                                 : k_wide_last_ws<8, 32, 8, true, 1, true, 4>;
     else if (teams == 2) k2 = b3 ? k_wide_last_ws<8, 32, 8, true, 2> : k_wide_last_ws<8, 32, 8, false, 2>;
     else if (gw == 8) k2 = nfi2 == 8 ? (b3 ? k_wide_last_ws<8, 32, 8, true> : kw32 ? k_wide_last_ws<8, 32, 8> : k_wide_last_ws<8, 0, 8>)
                                      : (kw32 ? k_wide_last_ws<4, 32, 8> : k_wide_last_ws<4, 0, 8>);
@@ -4670,7 +4927,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const bool l1s_k = k1 == k_wide_l1s<1, true> || k1 == k_wide_l1s<1, false> || k1 == k_wide_l1s<2, true> ||
                      k1 == k_wide_l1s<2, false> || k1 == k_wide_l1s<4, true> || k1 == k_wide_l1s<4, false>;
   if (ws2 && l1s_k && !(cte && std::strcmp(cte, "0") == 0)) a1.ctab = a2.ctab = reinterpret_cast<float*>(ws + W.ct);
-  const size_t lds2 = ws2 ? lds_ws : W.lds;
+  const size_t lds2 = ws2 ? lds_ws + (idx ? sizeof(int) * 3 * kIxInts : 0) : W.lds;
   const char* gwe0 = getenv("XPG_WIDE_GW");
   const int thr2 = ws2 ? 64 * ((gwe0 && atoi(gwe0) == 4 ? 4 : 8) + 4) : 256;
   const bool l1m = k1 == k_wide_l1m;

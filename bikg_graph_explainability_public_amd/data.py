@@ -48,7 +48,10 @@ def k_hop_subgraph(node_idx, num_hops, edge_index, num_nodes=None):
 def take_names(names, idx):
     """np.array(names, dtype=str)[idx].tolist() without converting every name: the selected
     names as numpy's str conversion gives them."""
-    return np.array([names[int(i)] for i in idx], dtype=str).tolist() if len(idx) else []
+    if not len(idx):
+        return []
+    ii = idx.tolist() if hasattr(idx, "tolist") else [int(i) for i in idx]  # one host copy
+    return np.array([names[i] for i in ii], dtype=str).tolist()
 
 
 def pad_feat_tensors(feat_tensors):

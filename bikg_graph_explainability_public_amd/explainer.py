@@ -84,6 +84,7 @@ class Explainer:
         self.edge_types = edge_types
         self.last_run = None  # diagnostics of the last run (per-repeat losses, path used)
         self.group = None     # torch.distributed process group for multi-GPU runs (None = world)
+        self._verified = set()  # module states whose compiled program passed verify_plan
 
     @property
     def edge_masks(self):
@@ -159,6 +160,15 @@ class Explainer:
         stack = torch.vstack(weights)
         std, mean = torch.std_mean(stack, 0, unbiased=False)
         return mean, std
+
+    def _verify_key(self, plan, c):
+        """What the compiled program's check depends on: the module object, every parameter
+        and buffer (storage and in-place version counter: an optimizer step or load_state_dict
+        changes them), the plan kind and the graph's type structure."""
+        state = tuple((t.data_ptr(), t._version) for t in self.arch.parameters())
+        bufs = tuple((t.data_ptr(), t._version) for t in self.arch.buffers())
+        return (id(self.arch), state, bufs, self.edge_masks, bool(getattr(plan, "multi_type", False)),
+                tuple(c["h_ntypes"] or ()), tuple(c["h_etypes"] or ()))
 
     # ------------------------------------------------------------------------------ run
     def prepare(self, element, device):
@@ -258,12 +268,26 @@ class Explainer:
             plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, [sub_ind], *geo)
             verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo)
         clock.mark("verify")
-        if plan is not None and self.params.get("verify_arch", True):
-            ok, err = verify()
-            if not ok:
-                warnings.warn(f"compiled arch disagrees with its torch forward (max err {err:.3g});"
-                              " using the generic torch path")
-                plan = None
+        arch_check = "off"
+        mode = self.params.get("verify_arch", True)
+        if plan is not None and mode:
+            # the check guards the arch lowering (program.compile_arch), which depends on the
+            # module and the graph's type structure, not on the query: once per module state
+            # (parameter storage + in-place version counters) and type structure per Explainer;
+            # params["verify_arch"] = "always" checks every run
+            key = self._verify_key(plan, c)
+            if mode == "always" or key not in self._verified:
+                ok, err = verify()
+                if not ok:
+                    warnings.warn(f"compiled arch disagrees with its torch forward (max err "
+                                  f"{err:.3g}); using the generic torch path")
+                    plan = None
+                    arch_check = "failed"
+                else:
+                    self._verified.add(key)
+                    arch_check = "verified"
+            else:
+                arch_check = "cached"
 
         clock.mark("sample")
         sampler = self.params.get("mask_sampler", "compat")
@@ -384,7 +408,7 @@ class Explainer:
         clock.mark("end")
         self.last_run = {"engine": plan is not None, "repeats": diag, "S": S,
                          "sub_ind": sub_ind, "plan": plan, "weights": config_vals,
-                         "phases": clock}
+                         "phases": clock, "arch_check": arch_check}
         return config_val_df, pathway_df
 
     def run_queries(self, elements, times=1):

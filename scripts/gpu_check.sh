@@ -40,6 +40,8 @@ for step in "$@"; do
     wsprof) run wsprof 700 bash scripts/ws_prof.sh ;;
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
     wsprof2) run wsprof2 600 bash scripts/ws_prof2.sh ;;
+    widetests) run widetests 600 python -u -m pytest tests/test_gpu_coverage.py tests/test_gpu_parity.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wide or c3 or hub" ;;
+    idxab) run idxab 600 python -u tools/ws_ab.py --variants "B3=1,IDX=0;B3=1;B3=1,IDX=0;B3=1;B3=1,RP=8;B3=1,RP=4" ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;
     profall) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profall -o run -- python3 bench.py --no-cpu-baseline ;;

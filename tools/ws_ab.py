@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bikg_graph_explainability_public_amd import _lib, engine, pipeline  # noqa: E402
 from bikg_graph_explainability_public_amd.nn import ConvStack  # noqa: E402
 
-KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW", "DBG", "PIPE", "RP", "CT")
+KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW", "DBG", "PIPE", "RP", "CT", "IDX")
 
 
 def set_env(spec):
@@ -48,6 +48,7 @@ def main():
     bits = engine.sample_shapley(13, args.rows, N, dev)
     print(f"plan N={N} E={E} F={F} in {time.time() - t0:.1f}s", flush=True)
     ref = None
+    first = None  # the first variant's output: later variants compared bitwise with it
     for spec in args.variants.split(";"):
         set_env(spec)
         y = plan.forward(bits)
@@ -64,7 +65,11 @@ def main():
             ref = plan.forward(bits).clone()
             set_env(spec)
         d = float((y - ref).abs().max())
-        print(f"[{spec:>18s}] {args.rows} rows: {ms:8.3f} ms  max|y - y_exact| = {d:.3e}", flush=True)
+        if first is None:
+            first = y.clone()
+        d1 = float((y - first).abs().max())
+        print(f"[{spec:>18s}] {args.rows} rows: {ms:8.3f} ms  max|y - y_exact| = {d:.3e}  "
+              f"max|y - y_first| = {d1:.3e}", flush=True)
     set_env("")
 
 
