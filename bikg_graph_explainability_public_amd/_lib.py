@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -73,6 +73,7 @@ _SIGS = {
     "xpg_sample_communities": ([ctypes.c_uint64, c_i64, c_i64, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp,
                                 c_vp, c_vp, c_vp], c_i32),
     "xpg_edge_keep": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
+    "xpg_rows_no_edge": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
     "xpg_popcount_rows": ([c_vp, c_i64, c_i64, c_vp, c_vp], c_i32),
     "xpg_shap_kernel": ([c_vp, c_i64, c_i64, c_vp, c_vp], c_i32),
     "xpg_dense": ([c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int,

@@ -410,6 +410,30 @@ __global__ void k_edge_keep(const uint32_t* __restrict__ bits, int64_t rows, int
 
 // ------------------------------------------------------------------------------------ KernelSHAP
 // one wave per row: lanes stride the row's words, popcount, wave-reduce.
+// Empty copies of the multi-node-type loop (model.py:213-215): out[r] = 1 iff mask row r keeps
+// no edge (both endpoints set).  One wave per row, 64 edges per round, the row's words read from
+// L1 / L2; the wave stops at the first round with a kept edge (most rows keep one early), so a
+// row costs a few rounds instead of the rows x edges keep matrix of k_edge_keep + a reduction.
+__global__ __launch_bounds__(256) void k_rows_no_edge(const uint32_t* __restrict__ bits, int64_t rows, int words,
+                                                      const int* __restrict__ src, const int* __restrict__ dst,
+                                                      int64_t n_edges, uint8_t* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;  // wave-uniform
+  const uint32_t* row = bits + r * words;
+  bool any = false;
+  for (int64_t e0 = 0; e0 < n_edges && !any; e0 += 64) {
+    const int64_t e = e0 + lane;
+    bool k = false;
+    if (e < n_edges) {
+      const int a = src[e], b = dst[e];
+      k = (((row[a >> 5] >> (a & 31)) & (row[b >> 5] >> (b & 31))) & 1u) != 0u;
+    }
+    any = __ballot(k) != 0ull;
+  }
+  if (lane == 0) out[r] = any ? 0 : 1;
+}
+
 __global__ void k_popcount(const uint32_t* __restrict__ bits, int64_t rows, int words,
                            int32_t* __restrict__ counts) {
   const int lane = threadIdx.x & 63;
@@ -575,16 +599,19 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
 // GCN self-loop / an empty SAGE neighbourhood).
 // Edge masks (deg_eid != NULL, Data.perturb_edge): every node is active and an in-edge counts iff
 // its own column bit is set.
-__global__ void k_degree(const uint32_t* __restrict__ bits, int64_t rows, int words, int n0,
+// n_deg: the F_0 prefix whose degrees are kept (kin [rows][n_rel][n_deg]): every F_0 node when
+// some term needs its sources' degrees (GCN) or edges carry the mask bits, else only the targets
+// (F_1, a prefix of F_0: k_agg then tests a MEAN source's own mask bit)
+__global__ void k_degree(const uint32_t* __restrict__ bits, int64_t rows, int words, int n0, int n_deg,
                          int n_rel, const int32_t* __restrict__ f0_node,
                          const int32_t* __restrict__ deg_ptr, const int32_t* __restrict__ deg_src,
                          const int32_t* __restrict__ deg_eid, float* __restrict__ kin) {
-  const int64_t per_row = (int64_t)n_rel * n0;
+  const int64_t per_row = (int64_t)n_rel * n_deg;
   int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (idx >= rows * per_row) return;
   const int64_t b = idx / per_row;
   const int rem = static_cast<int>(idx - b * per_row);
-  const int r = rem / n0, p = rem - r * n0;
+  const int r = rem / n_deg, p = rem - r * n_deg;
   const uint32_t* row = bits + b * words;
   const int* pp = deg_ptr + (int64_t)r * (n0 + 1);
   float out = -1.f;
@@ -630,6 +657,11 @@ struct AggArgs {
   const int32_t* agg_eid;
   const int32_t* self_ptr;
   const int32_t* self_eid;
+  // kin row pitch per relation (k_degree's n_deg); mbits / f0_node (non-null when kin holds only
+  // the targets' degrees): a MEAN source is active iff its own mask bit is set
+  int kpitch;
+  const uint32_t* mbits;
+  const int32_t* f0_node;
 };
 
 __device__ __forceinline__ float inv_sqrt_deg(float kin) {
@@ -656,7 +688,8 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
   if (item >= a.rows * a.n_tgt) return;
   const int64_t b = item / a.n_tgt;
   const int t = static_cast<int>(item - b * a.n_tgt);
-  const float* kb = a.kin + b * (int64_t)a.n_rel * a.n0;
+  const float* kb = a.kin + b * (int64_t)a.n_rel * a.kpitch;
+  const uint32_t* mrow = a.mbits ? a.mbits + b * a.words : nullptr;
   const int t0 = a.tgt_f0[t];
   const int tp = a.tgt_prev[t];
   float4 tot[NV];
@@ -679,7 +712,7 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
 #pragma unroll
       for (int j = 0; j < NV; ++j) s[j] = selfrow[sub + j * LPS];
     } else {
-      const float kt = kb[(int64_t)r * a.n0 + t0];
+      const float kt = kb[(int64_t)r * a.kpitch + t0];
       const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
       const uint32_t* brow = a.agg_eid ? a.bits + b * a.words : nullptr;
       if (kind == XPG_TERM_GCN) {
@@ -690,7 +723,7 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
         if (kt >= 0.f) {
           for (int e = pp[t]; e < pp[t + 1]; ++e) {
             const int u0 = a.agg_f0[e];
-            const float ku = kb[(int64_t)r * a.n0 + u0];
+            const float ku = kb[(int64_t)r * a.kpitch + u0];
             if (brow ? bit_of(brow, a.agg_eid[e]) : ku >= 0.f) {
               const float c = inv_sqrt_deg(ku) * dt;
               const int up = L1 ? u0 : a.agg_src[e];
@@ -714,7 +747,8 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
           for (int j = 0; j < NV; ++j) fma4(s[j], static_cast<float>(sm), selfrow[sub + j * LPS]);
           for (int e = pp[t]; e < pp[t + 1]; ++e) {
             const int u0 = a.agg_f0[e];
-            if (brow ? bit_of(brow, a.agg_eid[e]) : kb[(int64_t)r * a.n0 + u0] >= 0.f) {
+            if (brow ? bit_of(brow, a.agg_eid[e])
+                     : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f) {
               const int up = L1 ? u0 : a.agg_src[e];
               const float4* src = reinterpret_cast<const float4*>(base + (int64_t)up * a.width);
 #pragma unroll
@@ -4467,6 +4501,15 @@ bool plan_multi_type(const xpg_forward_plan* p) {
   return false;
 }
 
+// k_degree's kept prefix of F_0 (see k_degree): F_1 for plans without GCN terms or edge masks
+int deg_pitch(const xpg_forward_plan* p) {
+  if (p->edge_masks) return p->n0;
+  for (int l = 0; l < p->n_layers; ++l)
+    for (int k = 0; k < p->layers[l].n_terms; ++k)
+      if (p->layers[l].terms[k].kind == XPG_TERM_GCN) return p->n0;
+  return std::max(1, std::min(p->n0, p->layers[0].n_tgt));
+}
+
 struct WsLayout {
   size_t kin = 0, agg = 0, head0 = 0, head1 = 0, total = 0;
   size_t h[64];
@@ -4476,7 +4519,7 @@ int layout_ws(const xpg_forward_plan* p, int64_t rows, WsLayout* L) {
   XPG_REQ(p && p->n_layers >= 1 && p->n_layers <= 64, "plan: 1..64 conv layers required");
   size_t off = 0;
   L->kin = off;
-  off += align_up(sizeof(float) * (size_t)rows * p->n_rel * p->n0);
+  off += align_up(sizeof(float) * (size_t)rows * p->n_rel * deg_pitch(p));
   size_t agg_max = 0;
   for (int l = 0; l < p->n_layers; ++l) {
     const xpg_layer_desc& ly = p->layers[l];
@@ -5248,6 +5291,16 @@ int xpg_edge_keep(const uint32_t* bits, int64_t rows, int64_t cols, const int32_
   return XPG_OK;
 }
 
+int xpg_rows_no_edge(const uint32_t* bits, int64_t rows, int64_t cols, const int32_t* src, const int32_t* dst,
+                     int64_t n_edges, uint8_t* empty, xpg_stream_t stream) {
+  XPG_REQ(rows >= 0 && cols > 0 && n_edges >= 0, "rows_no_edge: bad shape");
+  if (rows == 0) return XPG_OK;
+  hipLaunchKernelGGL(k_rows_no_edge, dim3(static_cast<unsigned>(cdiv(rows, 4))), dim3(256), 0, S(stream), bits, rows,
+                     words_of(cols), src, dst, n_edges, empty);
+  XPG_LAUNCHED();
+  return XPG_OK;
+}
+
 int xpg_popcount_rows(const uint32_t* bits, int64_t rows, int64_t cols, int32_t* counts, xpg_stream_t stream) {
   XPG_REQ(rows >= 0 && cols > 0, "popcount: bad shape");
   if (rows == 0) return XPG_OK;
@@ -5359,11 +5412,12 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   char* ws = static_cast<char*>(workspace);
   float* kin = reinterpret_cast<float*>(ws + L.kin);
   const int words = words_of(p->cols);
+  const int kpitch = deg_pitch(p);
   {
-    const int64_t n = rows * (int64_t)p->n_rel * p->n0;
+    const int64_t n = rows * (int64_t)p->n_rel * kpitch;
     XPG_REQ(!p->edge_masks || p->deg_eid || p->n_deg_edges == 0, "masked_forward: edge-mask plan without deg_eid");
     hipLaunchKernelGGL(k_degree, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, st, bits, rows, words, p->n0,
-                       p->n_rel, p->f0_node, p->deg_ptr, p->deg_src, p->edge_masks ? p->deg_eid : nullptr, kin);
+                       kpitch, p->n_rel, p->f0_node, p->deg_ptr, p->deg_src, p->edge_masks ? p->deg_eid : nullptr, kin);
     XPG_LAUNCHED();
   }
   for (int l = 0; l < p->n_layers; ++l) {
@@ -5377,6 +5431,12 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
     a.n_tgt = ly.n_tgt;
     a.n_prev = l == 0 ? p->n0 : p->layers[l - 1].n_tgt;
     a.kin = kin;
+    a.kpitch = kpitch;
+    if (kpitch < p->n0) {  // kin holds the targets only: MEAN sources test their own bit
+      a.mbits = bits;
+      a.words = words;
+      a.f0_node = p->f0_node;
+    }
     a.tgt_prev = ly.tgt_prev;
     a.tgt_f0 = ly.tgt_f0;
     a.agg_ptr = ly.agg_ptr;

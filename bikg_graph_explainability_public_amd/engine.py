@@ -146,6 +146,19 @@ def edge_keep(bits, cols, src, dst):
     return keep.view(torch.bool)
 
 
+def rows_no_edge(bits, cols, src, dst):
+    """bool [rows]: mask rows that keep no edge (src[e], dst[e] both kept) — the multi-node-type
+    loop's empty copies (model.py:213-215), without the rows x edges keep matrix."""
+    _lib.require_device(bits, "bits")
+    rows = bits.shape[0]
+    s = src.to(device=bits.device, dtype=torch.int32).contiguous()
+    d = dst.to(device=bits.device, dtype=torch.int32).contiguous()
+    out = torch.empty(rows, dtype=torch.uint8, device=bits.device)
+    call("xpg_rows_no_edge", ptr(bits), rows, cols, ptr(s), ptr(d), s.numel(), ptr(out),
+         _lib.stream_of(bits.device))
+    return out.view(torch.bool)
+
+
 # ----------------------------------------------------------------------------- k-hop subgraph
 def khop_subgraph(node_idx: int, num_hops: int, edge_index: torch.Tensor, num_nodes: int):
     """Data.comp_graph's k_hop_subgraph (data.py:331-333; PyG 2.0.4 semantics, relabel_nodes=True,

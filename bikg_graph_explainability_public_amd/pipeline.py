@@ -125,19 +125,14 @@ def verify_edge_plan(plan, arch, feat, edge_index, u, v, rows=8, tol=1e-4):
     return err <= tol * max(1.0, ref.abs().max().item()), err
 
 
-def empty_copy_rows(bits, cols, edge_index, max_bytes=256 << 20):
+def empty_copy_rows(bits, cols, edge_index):
     """bool [rows]: mask rows that keep no edge of the (sub)graph — the reference's
     multi-node-type loop outputs 0 for such copies instead of running the model
-    (model.py:213-215).  Uses the HIP edge-keep kernel in row chunks."""
+    (model.py:213-215).  One HIP pass over the rows (engine.rows_no_edge)."""
     rows, E = bits.shape[0], edge_index.shape[1]
-    out = torch.ones(rows, dtype=torch.bool, device=bits.device)
     if E == 0:
-        return out
-    step = max(1, max_bytes // E)
-    for r0 in range(0, rows, step):
-        keep = engine.edge_keep(bits[r0:r0 + step], cols, edge_index[0], edge_index[1])
-        out[r0:r0 + step] = ~keep.view(-1, E).any(1)
-    return out
+        return torch.ones(rows, dtype=torch.bool, device=bits.device)
+    return engine.rows_no_edge(bits, cols, edge_index[0], edge_index[1])
 
 
 def multi_type_targets(y_rows, empty, batch, sub_ind, S, q4=True):

@@ -20,6 +20,8 @@
  *                                        Pathways.mask_generator (masks.py:81-194,
  *                                        pathways.py:234-385)
  *   xpg_edge_keep                      — Data.build_edge_mask        data.py:390-451
+ *   xpg_rows_no_edge                   — the empty-copy test of the multi-node-type loop
+ *                                        (a copy keeping no edge outputs 0)  model.py:213-215
  *   xpg_popcount_rows + xpg_shap_kernel— Kernel.compute             kernels.py:115-174
  *   xpg_masked_forward                 — Data.perturbator + Model.infer + extract_node_edge_output
  *                                        (wlm.py:349-436 -> data.py:591-648, model.py:62-116,
@@ -43,7 +45,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 13
+#define XPG_ABI_VERSION 14
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -96,6 +98,12 @@ int xpg_sample_communities(uint64_t seed, int64_t rows, int64_t cols, int32_t n_
 int xpg_edge_keep(const uint32_t* bits, int64_t rows, int64_t cols, const int32_t* src,
                   const int32_t* dst, int64_t n_edges, uint8_t* keep, xpg_stream_t stream);
 
+/* empty[r] = 1 iff mask row r keeps no edge (src[e] and dst[e] both set), else 0: the multi-node-type
+ * loop's copies without edges (model.py:213-215), one byte per row; stops at a row's first kept
+ * edge.  (ABI v14) */
+int xpg_rows_no_edge(const uint32_t* bits, int64_t rows, int64_t cols, const int32_t* src,
+                     const int32_t* dst, int64_t n_edges, uint8_t* empty, xpg_stream_t stream);
+
 /* ---------------------------------------------------------------- KernelSHAP */
 int xpg_popcount_rows(const uint32_t* bits, int64_t rows, int64_t cols, int32_t* counts,
                       xpg_stream_t stream);
@@ -134,7 +142,9 @@ typedef struct xpg_layer_desc {
   int32_t n_tgt;           /* |F_l|                                                    */
   int32_t n_edges;         /* agg_src / agg_f0 length (all relations)                  */
   const int32_t* tgt_prev; /* [n_tgt] position of each target inside F_{l-1}          */
-  const int32_t* tgt_f0;   /* [n_tgt] position of each target inside F_0               */
+  const int32_t* tgt_f0;   /* [n_tgt] position of each target inside F_0; frontiers are */
+                           /* prefix-ordered (F_l = the first |F_l| nodes of F_{l-1}),  */
+                           /* so every target of every layer sits in F_0[0, |F_1|)      */
   const int32_t* agg_ptr;  /* [n_rel * (n_tgt + 1)] in-edges per target, self-loops out */
   const int32_t* agg_src;  /* source positions inside F_{l-1}                          */
   const int32_t* agg_f0;   /* source positions inside F_0                              */

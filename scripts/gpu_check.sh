@@ -25,6 +25,10 @@ for step in "$@"; do
     # both ranks on cuda:0 (the driver's 8-GPU runs use RCCL, one GPU per rank)
     rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
     capture) run capture 400 python tools/capture_probe.py ;;
+    c5info) run c5info 300 python -u tools/c5_plan_info.py ;;
+    prof_*) sec=${step#prof_}
+           cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run prof_$sec 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$sec -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections $sec ;;
     # layer-2 ablations (c3 full size, one 32-row pass): full, no MFMA, no gathers, no epilogue,
     # exact f32 (B3=0) beside the default bf16x3
     wsdbg) run wsdbg 500 python tools/ws_ab.py --variants "B3=1;B3=1,DBG=16;B3=1,DBG=32;B3=1,DBG=64;B3=0" ;;
@@ -41,7 +45,7 @@ for step in "$@"; do
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
     wsprof2) run wsprof2 600 bash scripts/ws_prof2.sh ;;
     widetests) run widetests 600 python -u -m pytest tests/test_gpu_coverage.py tests/test_gpu_parity.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wide or c3 or hub" ;;
-    idxab) run idxab 600 python -u tools/ws_ab.py --variants "B3=1,IDX=0;B3=1;B3=1,IDX=0;B3=1;B3=1,RP=8;B3=1,RP=4" ;;
+    idxab) run idxab 600 python -u tools/ws_ab.py --variants "${IDXAB:-B3=1,IDX=0;B3=1;B3=1,IDX=0;B3=1;B3=1,RP=6}" ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;
     profall) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profall -o run -- python3 bench.py --no-cpu-baseline ;;

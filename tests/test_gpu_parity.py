@@ -89,6 +89,25 @@ def test_edge_keep_known_answer_and_random():
         np.testing.assert_array_equal(got, ref)
 
 
+def test_rows_no_edge_vs_edge_keep_oracle():
+    """xpg_rows_no_edge (the multi-node-type loop's empty copies, model.py:213-215) == no kept
+    edge in the oracle's edge mask, on sparse rows (many empty), all-off / all-on rows, edges
+    past the first 64-edge round, and an edge list of a single edge."""
+    e = _eng()
+    rng = np.random.default_rng(9)
+    for S, E, B, dens in [(50, 300, 40, 0.05), (1000, 5000, 70, 0.01), (700, 1, 20, 0.5),
+                          (3000, 200, 33, 0.03)]:
+        mm = rng.random((B, S)) < dens
+        mm[0] = False
+        mm[1] = True
+        eei = rng.integers(0, S, (2, E))
+        got = e.rows_no_edge(e.pack_masks(torch.as_tensor(mm).to(DEV)), S,
+                             torch.as_tensor(eei[0]), torch.as_tensor(eei[1])).cpu().numpy()
+        ref, _ = oracle.build_edge_mask(mm, eei)
+        np.testing.assert_array_equal(got, ~ref.reshape(B, E).any(1))
+        assert got[0] and not got[1]
+
+
 def test_perturb_node_seam():
     from bikg_graph_explainability_public_amd.data import Data
     m = torch.tensor([[1, 0, 1, 0, 1, 0, 1], [1, 1, 1, 1, 0, 0, 0], [0, 0, 0, 0, 1, 1, 1]],
