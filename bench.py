@@ -517,7 +517,7 @@ def headline(args, dev, world, rank, workload="c2"):
             graphs = []
             for b in range(2):
                 gph, outs = torch.cuda.CUDAGraph(), []
-                with torch.cuda.graph(gph):
+                with engine.capture_guard(), torch.cuda.graph(gph):
                     for j in range(unroll):
                         outs.append(pipe_step((b * unroll + j) & 1, stage[b][j] if ex else None))
                 graphs.append((gph, outs))
@@ -526,15 +526,15 @@ def headline(args, dev, world, rank, workload="c2"):
                 return sharding.all_gather_async(gath[b].view(-1), stage[b].view(-1))
         elif not split:
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+            with engine.capture_guard(), torch.cuda.graph(graph):
                 g_out = step(0, False, dev_seed=True)
         else:
             y_s = torch.empty(n_rows, dtype=torch.float32, device=dev)
             k_s = torch.empty(n_rows, dtype=torch.float64, device=dev)
             graph_a, graph_b = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph_a):
+            with engine.capture_guard(), torch.cuda.graph(graph_a):
                 g_bits, g_y, g_k = part_a(0, True)
-            with torch.cuda.graph(graph_b, pool=graph_a.pool()):
+            with engine.capture_guard(), torch.cuda.graph(graph_b, pool=graph_a.pool()):
                 g_w = part_b(0, True, g_bits, y_s, k_s)
                 seed_t.add_(1)
 

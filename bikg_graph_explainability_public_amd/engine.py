@@ -10,7 +10,9 @@ Plan (per query, built once per Explainer.run — DESIGN.md §3):
 
 All device memory is owned by torch tensors held by the plan; the C-ABI never allocates.
 """
+import contextlib
 import ctypes
+import gc
 import math
 
 import numpy as np
@@ -47,6 +49,26 @@ def unpack_masks(bits: torch.Tensor, cols: int) -> torch.Tensor:
     out = torch.empty((rows, cols), dtype=torch.uint8, device=bits.device)
     call("xpg_unpack_masks", ptr(bits), rows, cols, ptr(out), _lib.stream_of(bits.device))
     return out.view(torch.bool)
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """Wrap every HIP-graph capture of the hot path (`with capture_guard(), torch.cuda.graph(g)`).
+
+    Freeing a captured graph while another capture runs aborts the process on this HIP stack
+    (tools/capture_probe.py, variant graph_gc, profiles/r3_capture_probe.log: the round-2
+    `capture_end` crash of the pipelined bench).  A graph object reachable only from a reference
+    cycle is freed whenever Python's cyclic collector runs, which can be mid-capture; the guard
+    collects first and holds the collector off until the capture ends.  The graphs themselves
+    must stay referenced by the caller (the bench keeps them in a list)."""
+    gc.collect()
+    enabled = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if enabled:
+            gc.enable()
 
 
 def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0,

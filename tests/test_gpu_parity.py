@@ -151,7 +151,7 @@ def test_shapley_sampler_device_seed_and_graph_replay():
     e.sample_shapley_dev(seed_t, R, S)  # warm-up outside the capture
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with _eng().capture_guard(), torch.cuda.graph(g):
         out.copy_(e.sample_shapley_dev(seed_t, R, S))
         seed_t.add_(1)
     for s in (41, 42, 43):
@@ -403,7 +403,7 @@ def test_pipelined_prepared_fits_equal_eager():
     produce(sets[0])  # prologue: seed 700
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with _eng().capture_guard(), torch.cuda.graph(g):
         for j in range(2):
             pipe_step(j, snaps[j])
     for rep in range(3):
@@ -455,7 +455,7 @@ def test_captured_repeat_equals_eager():
     seed_t.fill_(300)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with _eng().capture_guard(), torch.cuda.graph(g):
         w_g = repeat(True)
     for s in (300, 301, 302):
         g.replay()

@@ -213,3 +213,29 @@ def test_community_columns_csr():
     ptr_, comm = community_columns([[0, 3, 4], [4, 5], [1]], 7)
     assert ptr_.tolist() == [0, 1, 2, 2, 3, 5, 6, 6]
     assert comm.tolist() == [0, 2, 0, 0, 1, 1]
+
+
+def test_capture_guard_holds_the_cyclic_collector():
+    """engine.capture_guard (wraps every HIP-graph capture): collects before, keeps Python's
+    cyclic GC off during the capture (a graph freed mid-capture aborts the process on this HIP
+    stack: tools/capture_probe.py graph_gc), restores it afterwards, also on an exception, and
+    leaves a caller's disabled collector disabled."""
+    import gc
+    from bikg_graph_explainability_public_amd import engine
+    assert gc.isenabled()
+    with engine.capture_guard():
+        assert not gc.isenabled()
+    assert gc.isenabled()
+    try:
+        with engine.capture_guard():
+            raise RuntimeError("capture failed")
+    except RuntimeError:
+        pass
+    assert gc.isenabled()
+    gc.disable()
+    try:
+        with engine.capture_guard():
+            assert not gc.isenabled()
+        assert not gc.isenabled()
+    finally:
+        gc.enable()
