@@ -789,6 +789,101 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
   }
 }
 
+// Layer-1 aggregation with lanes = mask rows (W = 32 or 64 features, no edge masks): wave = (block
+// of 64 mask rows, one target).  The tables are shared by every mask row, so each in-edge's table
+// row is a wave-uniform read (scalar loads) added to the lanes that keep the edge; only the
+// per-row keep bits / degrees are per-lane loads.  k_agg<true> instead gives each (row, target)
+// item 16 lanes that fetch every kept row's table slice themselves: for small frontiers and many
+// rows (the c5 shape) that re-reads the same few KB of table per mask row.  Same operations per
+// value in the same order as k_agg<true> (bitwise the same h1).
+template <int W>
+__global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
+  const int64_t wid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t nblk = (a.rows + 63) / 64;
+  if (wid >= nblk * a.n_tgt) return;  // wave-uniform
+  const int t = static_cast<int>(wid % a.n_tgt);
+  const int64_t b0 = (wid / a.n_tgt) * 64, b = b0 + lane;
+  const bool vrow = b < a.rows;
+  const int64_t bb = vrow ? b : b0;
+  const float* kb = a.kin + bb * (int64_t)a.n_rel * a.kpitch;
+  const uint32_t* mrow = a.mbits ? a.mbits + bb * a.words : nullptr;
+  const int t0 = a.tgt_f0[t];
+  float tot[W];
+#pragma unroll
+  for (int f = 0; f < W; ++f) tot[f] = 0.f;
+  for (int k = 0; k < a.n_terms; ++k) {
+    const int kind = a.kind[k];
+    const int r = a.rel[k];
+    if (a.tgt_type && a.dst_type[k] >= 0 && a.tgt_type[t] != a.dst_type[k]) continue;  // uniform
+    const float* __restrict__ T = a.table[k];
+    const float* __restrict__ selfrow = T + (int64_t)t0 * W;
+    float s[W];
+    if (kind == XPG_TERM_ROOT) {
+#pragma unroll
+      for (int f = 0; f < W; ++f) s[f] = selfrow[f];
+    } else {
+#pragma unroll
+      for (int f = 0; f < W; ++f) s[f] = 0.f;
+      const float kt = kb[(int64_t)r * a.kpitch + t0];
+      const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+      const int e0 = pp[t], e1 = pp[t + 1];
+      if (kind == XPG_TERM_GCN) {
+        const float dt = inv_sqrt_deg(kt);
+        const float cself = dt * dt;
+#pragma unroll
+        for (int f = 0; f < W; ++f) s[f] = fmaf(cself, selfrow[f], s[f]);
+        for (int e = e0; e < e1; ++e) {  // uniform
+          const int u0 = a.agg_f0[e];
+          const float ku = kb[(int64_t)r * a.kpitch + u0];
+          if (kt >= 0.f && ku >= 0.f) {
+            const float c = inv_sqrt_deg(ku) * dt;
+            const float* __restrict__ src = T + (int64_t)u0 * W;
+#pragma unroll
+            for (int f = 0; f < W; ++f) s[f] = fmaf(c, src[f], s[f]);
+          }
+        }
+      } else {  // MEAN
+        const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+        const float cnt = kt + static_cast<float>(sm);
+        if (kt >= 0.f) {
+#pragma unroll
+          for (int f = 0; f < W; ++f) s[f] = fmaf(static_cast<float>(sm), selfrow[f], s[f]);
+        }
+        for (int e = e0; e < e1; ++e) {  // uniform
+          const int u0 = a.agg_f0[e];
+          const bool keep = kt >= 0.f && (mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
+          if (keep) {
+            const float* __restrict__ src = T + (int64_t)u0 * W;
+#pragma unroll
+            for (int f = 0; f < W; ++f) s[f] += src[f];
+          }
+        }
+        if (kt >= 0.f) {
+          const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
+#pragma unroll
+          for (int f = 0; f < W; ++f) s[f] *= inv;
+        }
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < W; ++f) tot[f] += s[f];
+  }
+  if (!vrow) return;
+  float4* o = reinterpret_cast<float4*>(a.out + (b * a.n_tgt + t) * a.out_ld);
+  const float* bias = a.bias + (a.tgt_type ? (int64_t)a.tgt_type[t] * a.width : 0);
+#pragma unroll
+  for (int j = 0; j < W / 4; ++j) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int f = 4 * j + q;
+      v[q] = (f < a.f_real) ? act_apply(tot[f] + bias[f], a.act) : 0.f;
+    }
+    o[j] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 __global__ void k_take_col(const float* __restrict__ C, int64_t M, int64_t ldc, int col,
                            float* __restrict__ y) {
   int64_t m = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -4572,6 +4667,17 @@ int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t
 template <bool L1>
 int launch_agg(const AggArgs& a, hipStream_t st) {
   XPG_REQ(a.width % 32 == 0 && a.width > 0, "agg: row width must be a positive multiple of 32");
+  // layer 1, widths 32 / 64, no edge masks: lanes = mask rows (XPG_AGG_ROWS=0: k_agg)
+  const char* are = getenv("XPG_AGG_ROWS");
+  if (L1 && !a.agg_eid && (a.width == 32 || a.width == 64) && !(are && std::strcmp(are, "0") == 0)) {
+    const int64_t waves = cdiv(a.rows, 64) * a.n_tgt;
+    if (waves == 0) return XPG_OK;
+    const dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
+    if (a.width == 64) hipLaunchKernelGGL(k_agg_l1_rows<64>, grid, block, 0, st, a);
+    else hipLaunchKernelGGL(k_agg_l1_rows<32>, grid, block, 0, st, a);
+    XPG_LAUNCHED();
+    return XPG_OK;
+  }
   const int f4 = a.width / 4;  // float4 chunks per row (>= 8)
   const int lps = f4 >= 64 ? 64 : f4;
   const int nv = f4 / lps;

@@ -26,6 +26,7 @@ for step in "$@"; do
     rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
     capture) run capture 400 python tools/capture_probe.py ;;
     c5info) run c5info 300 python -u tools/c5_plan_info.py ;;
+    c5ab) XPG_AGG_ROWS=0 run c5_aggrows0 300 python bench.py --sections c5 --no-cpu-baseline && run c5_aggrows1 300 python bench.py --sections c5 --no-cpu-baseline && grep -h ms_per_job gpurun_out/c5_aggrows0.log gpurun_out/c5_aggrows1.log | python -c "import sys, json; [print(json.loads(l)['regimes']['c5_hetero']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     prof_*) sec=${step#prof_}
            cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run prof_$sec 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$sec -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections $sec ;;
