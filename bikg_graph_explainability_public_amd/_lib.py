@@ -72,6 +72,8 @@ _SIGS = {
     "xpg_sample_shapley_dev": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),
     "xpg_sample_communities": ([ctypes.c_uint64, c_i64, c_i64, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp,
                                 c_vp, c_vp, c_vp], c_i32),
+    "xpg_sample_communities_rows": ([ctypes.c_uint64, c_i64, c_i64, c_i64, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp,
+                                c_vp, c_vp, c_vp], c_i32),
     "xpg_edge_keep": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
     "xpg_rows_no_edge": ([c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp], c_i32),
     "xpg_popcount_rows": ([c_vp, c_i64, c_i64, c_vp, c_vp], c_i32),

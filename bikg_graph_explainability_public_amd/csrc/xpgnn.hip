@@ -278,7 +278,8 @@ __device__ uint32_t comm_permute(uint32_t x, uint32_t n, int hb, uint32_t k0, ui
 // LDS reads instead of two dependent L2 loads; the block plan is staged beside it.
 constexpr int kCommStageCols = 16384;
 template <bool SMALL, bool STAGED>
-__global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t rows, int64_t cols, int words,
+// row0: the launch writes global rows [row0, row0 + rows) to bits / prow rows 0.. (a rank's shard).
+__global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t row0, int64_t rows, int64_t cols, int words,
                                                      int n_comm, const int32_t* __restrict__ blocks,
                                                      int n_blocks, uint32_t src_rows, int hb, int shuffle,
                                                      const int32_t* __restrict__ col_ptr,
@@ -309,8 +310,8 @@ __global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t rows
     uint32_t src = 0u;
     int b = 0;
     if (active) {
-      src = shuffle ? comm_permute(static_cast<uint32_t>(r), src_rows, hb, k0 ^ 0x5EED1234u, k1 ^ 0x0F00D321u)
-                    : static_cast<uint32_t>(r);
+      const uint32_t rg = static_cast<uint32_t>(row0 + r);  // the global row
+      src = shuffle ? comm_permute(rg, src_rows, hb, k0 ^ 0x5EED1234u, k1 ^ 0x0F00D321u) : rg;
       int lo = 0, hi = n_blocks - 1;  // last block whose row_start <= src (wave-uniform)
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -5358,9 +5359,17 @@ int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, i
 int xpg_sample_communities(uint64_t seed, int64_t rows, int64_t cols, int32_t n_comm, const int32_t* blocks,
                            int32_t n_blocks, int64_t src_rows, int32_t shuffle, const int32_t* col_ptr,
                            const int32_t* col_comm, uint32_t* bits, int32_t* prow, xpg_stream_t stream) {
-  XPG_REQ(cols > 0 && rows >= 0 && n_comm > 0 && n_comm <= 32 * kCommMaxWords && n_blocks > 0 &&
-              n_blocks <= n_comm && src_rows >= rows && src_rows < (int64_t(1) << 31) && blocks && col_ptr &&
-              col_comm && bits,
+  return xpg_sample_communities_rows(seed, 0, rows, cols, n_comm, blocks, n_blocks, src_rows, shuffle, col_ptr,
+                                     col_comm, bits, prow, stream);
+}
+
+int xpg_sample_communities_rows(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, int32_t n_comm,
+                                const int32_t* blocks, int32_t n_blocks, int64_t src_rows, int32_t shuffle,
+                                const int32_t* col_ptr, const int32_t* col_comm, uint32_t* bits, int32_t* prow,
+                                xpg_stream_t stream) {
+  XPG_REQ(cols > 0 && rows >= 0 && row_offset >= 0 && n_comm > 0 && n_comm <= 32 * kCommMaxWords &&
+              n_blocks > 0 && n_blocks <= n_comm && src_rows >= row_offset + rows &&
+              src_rows < (int64_t(1) << 31) && blocks && col_ptr && col_comm && bits,
           "communities: bad shape");
   if (rows == 0) return XPG_OK;
   int nb = 1;  // bit length of src_rows - 1
@@ -5374,7 +5383,7 @@ int xpg_sample_communities(uint64_t seed, int64_t rows, int64_t cols, int32_t n_
   const int64_t want = std::min<int64_t>(cdiv(rows, 4), staged ? 2048 : 65536);
   const dim3 g(static_cast<unsigned>(want));
 #define XPG_COMM(SM, ST)                                                                                      \
-  hipLaunchKernelGGL((k_communities<SM, ST>), g, dim3(256), lds, S(stream), seed, rows, cols, words_of(cols), n_comm, \
+  hipLaunchKernelGGL((k_communities<SM, ST>), g, dim3(256), lds, S(stream), seed, row_offset, rows, cols, words_of(cols), n_comm, \
                      blocks, n_blocks, static_cast<uint32_t>(src_rows), hb, shuffle ? 1 : 0, col_ptr, col_comm, bits, \
                      prow)
   if (small) {

@@ -138,20 +138,25 @@ def community_tables(plan, communities, cols: int, device, columns=None):
 
 
 def sample_communities(seed: int, plan, communities, cols: int, device, columns=None,
-                       tables=None):
+                       tables=None, row_offset: int = 0, rows: int = None):
     """Device community masks (masks.py:81-194, pathways.py:234-385).
 
     plan = Mask.community_plan(); columns = community_columns(communities, cols); tables =
     community_tables(...) (skips the per-call uploads).  Returns (row bits int32 [rows, words],
-    pathway_rows int32 [rows])."""
+    pathway_rows int32 [rows]).  row_offset / rows: only the global rows [row_offset,
+    row_offset + rows) of the repeat (a rank's shard; the same rows as the full call's)."""
     if tables is None:
         tables = community_tables(plan, communities, cols, device, columns)
-    blocks, col_ptr, col_comm, src_rows, rows, shuffle, n_comm, cols = tables
+    blocks, col_ptr, col_comm, src_rows, total, shuffle, n_comm, cols = tables
+    rows = total - row_offset if rows is None else rows
+    if row_offset < 0 or rows < 0 or row_offset + rows > total:
+        raise ValueError(f"community rows [{row_offset}, {row_offset + rows}) outside the "
+                         f"repeat's {total} rows")
     dev = blocks.device
     bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=dev)
     prow = torch.empty(rows, dtype=torch.int32, device=dev)
-    call("xpg_sample_communities", ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), rows, cols,
-         n_comm, ptr(blocks), blocks.shape[0], src_rows, int(shuffle),
+    call("xpg_sample_communities_rows", ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), row_offset,
+         rows, cols, n_comm, ptr(blocks), blocks.shape[0], src_rows, int(shuffle),
          ptr(col_ptr), ptr(col_comm), ptr(bits), ptr(prow), _lib.stream_of(dev))
     return bits, prow
 

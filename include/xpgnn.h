@@ -92,6 +92,13 @@ int xpg_sample_communities(uint64_t seed, int64_t rows, int64_t cols, int32_t n_
                            const int32_t* blocks, int32_t n_blocks, int64_t src_rows,
                            int32_t shuffle, const int32_t* col_ptr, const int32_t* col_comm,
                            uint32_t* bits, int32_t* prow, xpg_stream_t stream);
+/* the same rows' global range [row_offset, row_offset + rows) only, written to bits / prow from row 0
+ * (row r of the full call == row r - row_offset here): a rank generates its own shard (ABI v14) */
+int xpg_sample_communities_rows(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,
+                                int32_t n_comm, const int32_t* blocks, int32_t n_blocks,
+                                int64_t src_rows, int32_t shuffle, const int32_t* col_ptr,
+                                const int32_t* col_comm, uint32_t* bits, int32_t* prow,
+                                xpg_stream_t stream);
 
 /* ---------------------------------------------------------------- perturbation */
 /* keep[b*n_edges + e] = bit(b, src[e]) & bit(b, dst[e])   (data.py:420-449) */

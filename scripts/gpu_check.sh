@@ -25,6 +25,7 @@ for step in "$@"; do
     # both ranks on cuda:0 (the driver's 8-GPU runs use RCCL, one GPU per rank)
     rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
     capture) run capture 400 python tools/capture_probe.py ;;
+    rank2c5) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2c5 500 python bench.py --gpus 2 --sections c5 --no-cpu-baseline && run rank1c5 300 python bench.py --sections c5 --no-cpu-baseline && grep -h result_checksum gpurun_out/rank2c5.log gpurun_out/rank1c5.log | python -c "import sys, json; [print(json.loads(l)['n_gpus'], json.loads(l)['regimes']['c5_hetero']['result_checksum'], json.loads(l)['regimes']['c5_hetero']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     c5info) run c5info 300 python -u tools/c5_plan_info.py ;;
     c5ab) XPG_AGG_ROWS=0 run c5_aggrows0 300 python bench.py --sections c5 --no-cpu-baseline && run c5_aggrows1 300 python bench.py --sections c5 --no-cpu-baseline && grep -h ms_per_job gpurun_out/c5_aggrows0.log gpurun_out/c5_aggrows1.log | python -c "import sys, json; [print(json.loads(l)['regimes']['c5_hetero']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     prof_*) sec=${step#prof_}

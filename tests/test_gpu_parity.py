@@ -226,8 +226,17 @@ def test_community_sampler_structure(S, lens, samples):
     assert torch.equal(sb, sb2)
     sb3, _ = e.sample_communities(6, (blocks, src_rows, src_rows, True), pathways, S, DEV)
     assert not torch.equal(sb, sb3)
-    tb, _ = e.sample_communities(5, plan, pathways, S, DEV)
+    tb, tp = e.sample_communities(5, plan, pathways, S, DEV)
     assert tb.shape[0] == rows
+    # a rank's shard: rows [a, b) of the repeat == the same rows of the full call (shuffled and
+    # truncated plans), the pathway rows too
+    for a_, b_ in [(0, 1), (rows // 3, rows // 3 + 5), (rows - 7, rows), (1, rows)]:
+        if not 0 <= a_ < b_ <= rows:
+            continue
+        pb, pp = e.sample_communities(5, plan, pathways, S, DEV, row_offset=a_, rows=b_ - a_)
+        assert torch.equal(pb, tb[a_:b_]) and torch.equal(pp, tp[a_:b_])
+    with pytest.raises(ValueError):
+        e.sample_communities(5, plan, pathways, S, DEV, row_offset=rows - 1, rows=2)
 
 
 def test_community_sampler_dead_mask_and_overlap():
