@@ -2455,6 +2455,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   }
   if (PIPE && IDX && wave < GW) {
     // ------------------------------------------------------------------ gather role, shared lists
+    if (a.dbg & 256) __builtin_amdgcn_s_setprio(2);  // (experiment) gather waves issue first
     const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
     const int s0 = g;
     const bool v0 = s0 < a.nr;
@@ -2971,6 +2972,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     }
   } else {
     // ------------------------------------------------------------------ MFMA role
+    if (a.dbg & 512) __builtin_amdgcn_s_setprio(2);  // (experiment) MFMA waves issue first
     const int nb = wave - GW, i32 = lane & 31, h = lane >> 5;
     const bool active = nb * 32 < a.f_out_pad;
     const int col = nb * 32 + i32;

@@ -427,14 +427,26 @@ class ForwardPlan:
 
         self._layers = (LayerDesc * L)()
         prev_pad = None
+        self.terms_kept = []  # per layer: terms after dropping other node types' relations
         for li, conv in enumerate(program.convs):
             lvl = li + 1
             n_t = fr[lvl].size
             f_out_pad = _rup(conv.f_out, 32)
             if f_out_pad > 256 or len(conv.terms) > _lib.MAX_TERMS:
                 raise ValueError("conv wider than 256 or more than 8 terms is not supported")
+            terms = list(conv.terms)
+            if nt_np is not None:
+                # every target of this layer has one node type: a relation term of another
+                # destination type adds exactly 0 to every target (HeteroConv sums per
+                # destination), so it is dropped — fewer aggregate columns and a shorter K of
+                # the layer's dense product (the query layer of a multi-type plan)
+                tt = np.unique(nt_np[fr[lvl]])
+                if tt.size == 1:
+                    kept = [t for t in terms if t.dst_type < 0 or t.dst_type == int(tt[0])]
+                    terms = kept or terms
+            self.terms_kept.append(len(terms))
             ld = self._layers[li]
-            ld.n_terms = len(conv.terms)
+            ld.n_terms = len(terms)
             ld.act = ACT[conv.act]
             ld.f_out = conv.f_out
             ld.f_out_pad = f_out_pad
@@ -460,12 +472,12 @@ class ForwardPlan:
             ld.bias = bias.data_ptr()
             ld.n_types = n_types
             ld.tgt_type = self._i32(nt_np[fr[lvl]]).data_ptr() if nt_np is not None else None
-            for k, term in enumerate(conv.terms):
+            for k, term in enumerate(terms):
                 ld.terms[k].kind = TERM[term.kind]
                 ld.terms[k].rel = term.rel
                 ld.terms[k].dst_type = term.dst_type
             if li == 0:
-                for k, term in enumerate(conv.terms):
+                for k, term in enumerate(terms):
                     T = dense(X0, term.weight.to(device), None, None)
                     Tp = torch.zeros((n0, f_out_pad), dtype=torch.float32, device=device)
                     Tp[:, :conv.f_out] = T
@@ -473,9 +485,9 @@ class ForwardPlan:
                     ld.terms[k].table = Tp.data_ptr()
                 ld.weight = None
             else:
-                kt = len(conv.terms) * prev_pad
+                kt = len(terms) * prev_pad
                 Wc = torch.zeros((f_out_pad, kt), dtype=torch.float32, device=device)
-                for k, term in enumerate(conv.terms):
+                for k, term in enumerate(terms):
                     Wc[:conv.f_out, k * prev_pad:k * prev_pad + conv.f_in] = term.weight.to(device)
                 self._keep.append(Wc)
                 ld.weight = Wc.data_ptr()
