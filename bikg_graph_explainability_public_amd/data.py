@@ -11,11 +11,11 @@
 import itertools
 
 import numpy as np
-import pandas as pd
 import torch
 import torch.nn.functional as F
 
 from . import engine
+from .frames import sorted_frame
 
 
 def k_hop_subgraph(node_idx, num_hops, edge_index, num_nodes=None):
@@ -236,7 +236,6 @@ class Data:
     @staticmethod
     def config_val_dataframe(config_val_mean, config_val_std, names):
         """data.py:651-693."""
-        df = pd.DataFrame({"name": names,
-                           "config_value_mean": config_val_mean.detach().cpu().numpy(),
-                           "config_value_std": config_val_std.detach().cpu().numpy()})
-        return df.set_index("name").sort_values(by=["config_value_mean"], ascending=False)
+        return sorted_frame(names, {"config_value_mean": config_val_mean.detach().cpu().numpy(),
+                                    "config_value_std": config_val_std.detach().cpu().numpy()},
+                            "config_value_mean")

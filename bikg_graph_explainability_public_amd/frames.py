@@ -1,0 +1,27 @@
+"""Result tables: the reference's `pd.DataFrame({...}).set_index("name").sort_values(by=[key],
+ascending=False)` (data.py:651-693, pathways.py:420-429, the latter + `.dropna()`), built once from
+numpy arrays instead of through three intermediate frames.  The row order is pandas' own
+single-key sort (pandas.core.sorting.nargsort: NaN rows set aside, non-NaN values reversed,
+quicksort argsort, reversed back, NaN rows appended in their original order), so ties and NaNs
+come out exactly where pandas puts them."""
+import numpy as np
+import pandas as pd
+
+
+def sorted_frame(names, columns, key, dropna=False):
+    """names: row labels (index "name"); columns: {column: 1-D array} in output order; rows
+    sorted by `key` descending; dropna drops every row with a NaN in any column."""
+    cols = {c: np.asarray(v) for c, v in columns.items()}
+    s = cols[key]
+    nan = np.isnan(s) if s.dtype.kind == "f" else np.zeros(len(s), dtype=bool)
+    pos = np.arange(len(s))
+    nn, ni = s[~nan][::-1], pos[~nan][::-1]
+    order = np.concatenate([ni[nn.argsort(kind="quicksort")][::-1], pos[nan]])
+    if dropna:
+        bad = np.zeros(len(s), dtype=bool)
+        for v in cols.values():
+            if v.dtype.kind == "f":
+                bad |= np.isnan(v)
+        order = order[~bad[order]]
+    index = pd.Index(list(names), name="name")[order]
+    return pd.DataFrame({c: v[order] for c, v in cols.items()}, index=index)

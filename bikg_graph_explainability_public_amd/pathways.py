@@ -12,6 +12,8 @@ import numpy as np
 import pandas as pd
 import torch
 
+from .frames import sorted_frame
+
 
 class Pathways:
     """Graph communities.  communities: list of lists of names or indices (or a dict per
@@ -125,16 +127,26 @@ class Pathways:
     def aggregate(self, config_val, community_inds):
         """pathways.py:387-429 — community score = mean member score; DataFrame indexed by
         community name, sorted descending, NaN rows dropped.  One segmented mean (index_add)
-        on the scores' device, one host transfer."""
+        on the scores' device (member / segment index tensors cached while the communities are
+        unchanged), one host transfer, and the frame built once from the sorted arrays."""
         dev = config_val.device
-        lens = [len(c) for c in community_inds]
-        flat = torch.tensor(list(itertools.chain.from_iterable(community_inds)),
-                            dtype=torch.long, device=dev)
-        seg = torch.repeat_interleave(torch.arange(len(lens), device=dev),
-                                      torch.tensor(lens, device=dev))
+        flat, seg, cnt = self._segments(community_inds, dev)
         vals = config_val.reshape(-1).float()[flat]
-        sums = torch.zeros(len(lens), dtype=torch.float32, device=dev).index_add_(0, seg, vals)
-        cnt = torch.tensor(lens, dtype=torch.float32, device=dev)
-        scores = (sums / cnt).cpu().tolist()
-        df = pd.DataFrame({"name": self.community_names, "score": scores}).set_index("name")
-        return df.sort_values(by=["score"], ascending=False).dropna()
+        sums = torch.zeros(cnt.numel(), dtype=torch.float32, device=dev).index_add_(0, seg, vals)
+        scores = (sums / cnt).cpu().numpy().astype(np.float64)
+        return sorted_frame(self.community_names, {"score": scores}, "score", dropna=True)
+
+    def _segments(self, community_inds, dev):
+        lens = np.fromiter((len(c) for c in community_inds), dtype=np.int64,
+                           count=len(community_inds))
+        flat = np.fromiter(itertools.chain.from_iterable(community_inds), dtype=np.int64,
+                           count=int(lens.sum()))
+        c = getattr(self, "_seg_cache", None)
+        if c is not None and c[0] == dev and np.array_equal(c[1], lens) and np.array_equal(c[2], flat):
+            return c[3]
+        seg = np.repeat(np.arange(len(lens), dtype=np.int64), lens)
+        t = (torch.from_numpy(flat).to(dev), torch.from_numpy(seg).to(dev),
+             torch.from_numpy(lens.astype(np.float32)).to(dev))
+        self._seg_cache = (dev, lens, flat, t)
+        return t
+
