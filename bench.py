@@ -993,14 +993,13 @@ def c5_section(args, dev, world, rank):
 
     def rows_of(step_seed, lo, hi):
         """global mask rows [lo, hi) of the job (repeat i = seed step_seed * 100 + i)"""
-        parts = []
+        buf = torch.empty((hi - lo, (S + 31) // 32), dtype=torch.int32, device=dev)
         for i in range(lo // R, (hi - 1) // R + 1 if hi > lo else lo // R):
             a_, b_ = max(lo, i * R) - i * R, min(hi, (i + 1) * R) - i * R
-            parts.append(engine.sample_communities(step_seed * 100 + i, cplan, pathways, S, dev,
-                                                   tables=tabs, row_offset=a_, rows=b_ - a_)[0])
-        if not parts:
-            return torch.empty((0, (S + 31) // 32), dtype=torch.int32, device=dev)
-        return parts[0] if len(parts) == 1 else torch.cat(parts)
+            engine.sample_communities(step_seed * 100 + i, cplan, pathways, S, dev, tables=tabs,
+                                      row_offset=a_, rows=b_ - a_,
+                                      out=buf[i * R + a_ - lo:i * R + b_ - lo])
+        return buf
 
     def job(step_seed, record):
         marks = [torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]

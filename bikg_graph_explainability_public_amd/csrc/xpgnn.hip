@@ -521,27 +521,34 @@ __global__ void k_shap_approx_rows(const int32_t* __restrict__ cnt, int64_t rows
 }
 
 // pass 2 (one block): the reference's loop `while sum(kernel) == 0 and ref > 0` (kernels.py:
-// 148-162) — normally one sum test; the ref = int(0.9 ref) back-off recomputes rows in-block —
-// then +-inf / NaN -> 0 (kernels.py:172).
+// 148-162).  Every row value is >= 0 or +inf (M > 0, choose > 0, 0 <= k <= M), so the sum is > 0
+// exactly when some value is > 0: the block scans 1024-row chunks until one holds a positive
+// value (normally the first), instead of summing every row; the ref = int(0.9 ref) back-off
+// recomputes rows in-block.
 __global__ __launch_bounds__(1024) void k_shap_approx_finish(const int32_t* __restrict__ cnt,
                                                              int64_t rows, int64_t cols,
                                                              double* __restrict__ out) {
-  __shared__ double red[16];
   const int64_t Mi = cols - 1;
   int ref = 1000;
   for (;;) {
-    double part = 0.0;
-    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) part += out[r];
-    const double sum = block_sum_d(part, red);
-    if (sum > 0.0) break;
+    bool found = false;
+    for (int64_t base = 0; base < rows && !found; base += blockDim.x) {  // block-uniform
+      const int64_t r = base + threadIdx.x;
+      found = __syncthreads_or(r < rows && out[r] > 0.0) != 0;
+    }
+    if (found) break;
     ref = static_cast<int>(0.9 * static_cast<double>(ref));
-    if (!(sum == 0.0 && ref > 0)) break;
+    if (!(ref > 0)) break;  // the sum is 0 here
     __syncthreads();
     for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) out[r] = shap_approx_row(cnt[r], Mi, ref);
     __syncthreads();
   }
-  __syncthreads();
-  for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) out[r] = clean_inf(out[r]);
+}
+
+// pass 3 (grid): +-inf / NaN -> 0 (kernels.py:172)
+__global__ void k_shap_clean(int64_t rows, double* __restrict__ out) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r < rows) out[r] = clean_inf(out[r]);
 }
 
 // ------------------------------------------------------------------------------------ dense
@@ -5437,6 +5444,9 @@ int xpg_shap_kernel(const int32_t* counts, int64_t rows, int64_t cols, double* k
                        counts, rows, cols, kernel_out);
     XPG_LAUNCHED();
     hipLaunchKernelGGL(k_shap_approx_finish, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
+    XPG_LAUNCHED();
+    hipLaunchKernelGGL(k_shap_clean, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream), rows,
+                       kernel_out);
   }
   XPG_LAUNCHED();
   return XPG_OK;

@@ -138,13 +138,15 @@ def community_tables(plan, communities, cols: int, device, columns=None):
 
 
 def sample_communities(seed: int, plan, communities, cols: int, device, columns=None,
-                       tables=None, row_offset: int = 0, rows: int = None):
+                       tables=None, row_offset: int = 0, rows: int = None, out=None):
     """Device community masks (masks.py:81-194, pathways.py:234-385).
 
     plan = Mask.community_plan(); columns = community_columns(communities, cols); tables =
     community_tables(...) (skips the per-call uploads).  Returns (row bits int32 [rows, words],
     pathway_rows int32 [rows]).  row_offset / rows: only the global rows [row_offset,
-    row_offset + rows) of the repeat (a rank's shard; the same rows as the full call's)."""
+    row_offset + rows) of the repeat (a rank's shard; the same rows as the full call's).  out:
+    a contiguous int32 [rows, words] view to write the bits into (e.g. one repeat's slice of a
+    multi-repeat buffer, instead of a torch.cat of per-repeat draws)."""
     if tables is None:
         tables = community_tables(plan, communities, cols, device, columns)
     blocks, col_ptr, col_comm, src_rows, total, shuffle, n_comm, cols = tables
@@ -153,7 +155,14 @@ def sample_communities(seed: int, plan, communities, cols: int, device, columns=
         raise ValueError(f"community rows [{row_offset}, {row_offset + rows}) outside the "
                          f"repeat's {total} rows")
     dev = blocks.device
-    bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=dev)
+    if out is None:
+        bits = torch.empty((rows, words_of(cols)), dtype=torch.int32, device=dev)
+    else:
+        if (out.dtype != torch.int32 or tuple(out.shape) != (rows, words_of(cols))
+                or not out.is_contiguous() or out.device != dev):
+            raise ValueError(f"out must be a contiguous int32 [{rows}, {words_of(cols)}] tensor "
+                             f"on {dev}")
+        bits = out
     prow = torch.empty(rows, dtype=torch.int32, device=dev)
     call("xpg_sample_communities_rows", ctypes.c_uint64(int(seed) & (2 ** 64 - 1)), row_offset,
          rows, cols, n_comm, ptr(blocks), blocks.shape[0], src_rows, int(shuffle),

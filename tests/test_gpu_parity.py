@@ -235,6 +235,13 @@ def test_community_sampler_structure(S, lens, samples):
             continue
         pb, pp = e.sample_communities(5, plan, pathways, S, DEV, row_offset=a_, rows=b_ - a_)
         assert torch.equal(pb, tb[a_:b_]) and torch.equal(pp, tp[a_:b_])
+    # out=: written in place into a slice of a bigger buffer, the rows around it untouched
+    big = torch.full((rows + 6, tb.shape[1]), -7, dtype=torch.int32, device=DEV)
+    ob, _ = e.sample_communities(5, plan, pathways, S, DEV, out=big[3:3 + rows])
+    assert ob.data_ptr() == big[3].data_ptr() and torch.equal(big[3:3 + rows], tb)
+    assert bool((big[:3] == -7).all()) and bool((big[3 + rows:] == -7).all())
+    with pytest.raises(ValueError):
+        e.sample_communities(5, plan, pathways, S, DEV, out=big[:rows, :-1])
     with pytest.raises(ValueError):
         e.sample_communities(5, plan, pathways, S, DEV, row_offset=rows - 1, rows=2)
 
