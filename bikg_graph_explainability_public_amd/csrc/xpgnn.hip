@@ -276,8 +276,14 @@ __device__ uint32_t comm_permute(uint32_t x, uint32_t n, int hb, uint32_t k0, ui
 // STAGED (cols <= kCommStageCols): each workgroup first stages every column's community as one
 // int16 in LDS (-1: none, -2: several -> the CSR in global memory), so the per-slice lookups are
 // LDS reads instead of two dependent L2 loads; the block plan is staged beside it.
+// CM (SMALL and STAGED, n_comm x words fit LDS): the staging builds one column bitmask per
+// community instead (cm[j] = the columns of community j), and a row is assembled a word per lane:
+// OR of the active communities' masks outside the own community, the own community's columns
+// from the internal random word -- the same bits as the per-column rule (a column of several
+// communities: internal bit when it is in the own one, else the OR of its communities' flags),
+// for ~10 LDS reads per word instead of a lookup + ballot per 64 columns.
 constexpr int kCommStageCols = 16384;
-template <bool SMALL, bool STAGED>
+template <bool SMALL, bool STAGED, bool CM = false>
 // row0: the launch writes global rows [row0, row0 + rows) to bits / prow rows 0.. (a rank's shard).
 __global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t row0, int64_t rows, int64_t cols, int words,
                                                      int n_comm, const int32_t* __restrict__ blocks,
@@ -292,12 +298,20 @@ __global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t row0
   uint32_t* lflags = comm_lds;
   int32_t* lblk = reinterpret_cast<int32_t*>(comm_lds + (SMALL ? 0 : 4 * fw));
   int16_t* lone = reinterpret_cast<int16_t*>(lblk + (STAGED ? 5 * n_blocks : 0));
+  uint32_t* cm = reinterpret_cast<uint32_t*>(lblk + (STAGED ? 5 * n_blocks : 0));  // CM: [n_comm][words]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (STAGED) {
+  if (CM) {
+    for (int i = threadIdx.x; i < n_comm * words; i += blockDim.x) cm[i] = 0u;
+    __syncthreads();
+    for (int c = threadIdx.x; c < cols; c += blockDim.x)
+      for (int i = col_ptr[c]; i < col_ptr[c + 1]; ++i) atomicOr(&cm[col_comm[i] * words + (c >> 5)], 1u << (c & 31));
+  } else if (STAGED) {
     for (int c = threadIdx.x; c < cols; c += blockDim.x) {
       const int p0 = col_ptr[c], n = col_ptr[c + 1] - p0;
       lone[c] = static_cast<int16_t>(n == 0 ? -1 : (n == 1 ? col_comm[p0] : -2));
     }
+  }
+  if (STAGED) {
     for (int i = threadIdx.x; i < 5 * n_blocks; i += blockDim.x) lblk[i] = blocks[i];
     __syncthreads();
     blocks = lblk;
@@ -351,7 +365,23 @@ __global__ __launch_bounds__(256) void k_communities(uint64_t seed, int64_t row0
       extra = static_cast<int>(pick);
     }
     if (!SMALL) __syncthreads();
-    if (active) {
+    if (CM && active) {
+      uint64_t act = f64 & ~(own >= 0 ? 1ull << own : 0ull);
+      if (extra >= 0 && extra != own) act |= 1ull << extra;
+      uint32_t* dst = bits + r * words;
+      for (int w0 = 0; w0 < words; w0 += 64) {  // uniform
+        const int w = w0 + lane;
+        // internal word w: the per-column path's Philox word for columns 32 w .. 32 w + 31
+        const uint32_t iw = philox4x32_10(make_uint4(static_cast<uint32_t>(w), src, 0u, 0x494E5431u), k0, k1).x;
+        if (w < words) {
+          uint32_t acc = 0u;
+          for (uint64_t m = act; m; m &= m - 1) acc |= cm[(__builtin_ctzll(m)) * words + w];  // uniform
+          const uint32_t mine = own >= 0 ? cm[own * words + w] : 0u;
+          dst[w] = (acc & ~mine) | (iw & mine);
+        }
+      }
+      if (lane == 0 && prow) prow[r] = own;
+    } else if (active) {
       uint64_t keep = 0;
       const int slices = static_cast<int>((cols + 63) >> 6);
       uint32_t* dst = bits + r * words;
@@ -5388,14 +5418,24 @@ int xpg_sample_communities_rows(uint64_t seed, int64_t row_offset, int64_t rows,
   const size_t flag_bytes = small ? 0 : sizeof(uint32_t) * 4 * static_cast<size_t>((n_comm + 31) / 32);
   const size_t stage_bytes = sizeof(int32_t) * 5 * static_cast<size_t>(n_blocks) + sizeof(int16_t) * static_cast<size_t>(cols);
   const bool staged = cols <= kCommStageCols && flag_bytes + stage_bytes <= 64 * 1024;
-  const size_t lds = flag_bytes + (staged ? stage_bytes : 0);
-  const int64_t want = std::min<int64_t>(cdiv(rows, 4), staged ? 2048 : 65536);
+  const char* cmo = getenv("XPG_COMM_CM");
+  const bool cmode = small && cols <= kCommStageCols && sizeof(int32_t) * (5 * static_cast<size_t>(n_blocks) +
+                     static_cast<size_t>(n_comm) * words_of(cols)) <= 48 * 1024 && !(cmo && std::strcmp(cmo, "0") == 0);
+  const size_t lds = cmode ? sizeof(int32_t) * (5 * static_cast<size_t>(n_blocks) + static_cast<size_t>(n_comm) * words_of(cols))
+                           : flag_bytes + (staged ? stage_bytes : 0);
+  const char* cb = getenv("XPG_COMM_BLOCKS");
+  const int64_t cap = cb ? std::max(1, atoi(cb)) : (staged ? 2048 : 65536);
+  const int64_t want = std::min<int64_t>(cdiv(rows, 4), cap);
   const dim3 g(static_cast<unsigned>(want));
 #define XPG_COMM(SM, ST)                                                                                      \
   hipLaunchKernelGGL((k_communities<SM, ST>), g, dim3(256), lds, S(stream), seed, row_offset, rows, cols, words_of(cols), n_comm, \
                      blocks, n_blocks, static_cast<uint32_t>(src_rows), hb, shuffle ? 1 : 0, col_ptr, col_comm, bits, \
                      prow)
-  if (small) {
+  if (cmode) {
+    hipLaunchKernelGGL((k_communities<true, true, true>), g, dim3(256), lds, S(stream), seed, row_offset, rows, cols,
+                       words_of(cols), n_comm, blocks, n_blocks, static_cast<uint32_t>(src_rows), hb, shuffle ? 1 : 0,
+                       col_ptr, col_comm, bits, prow);
+  } else if (small) {
     if (staged) XPG_COMM(true, true); else XPG_COMM(true, false);
   } else {
     if (staged) XPG_COMM(false, true); else XPG_COMM(false, false);
