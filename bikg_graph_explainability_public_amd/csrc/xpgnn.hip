@@ -1669,7 +1669,8 @@ struct WideArgs {
   int64_t rstride;  // floats between consecutive source rows: w_row (tables) or 32 w_row (h1)
   int head1;  // the head is one Linear(f_out, 1) (+ act) read at column 0: fused epilogue
   int dbg;   // diagnostics (XPG_WIDE_DBG): 1 skip dense + head, 2 skip row gathers, 4 head, 8 dense;
-             // warp-specialised layer 2: 16 no MFMA, 32 no gathers, 64 no epilogue, 128 no products
+             // warp-specialised layer 2: 16 no MFMA, 32 no gathers, 64 no epilogue, 128 no products,
+             // 512 MFMA waves without the raised issue priority
   int K, a_ld, f_out, f_out_pad, n_head, out_col, h_ld, o_h0, o_h1, o_e;
   int o_hw[kFusedMaxHead];
   const uint32_t* mT0;
@@ -2492,7 +2493,6 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   }
   if (PIPE && IDX && wave < GW) {
     // ------------------------------------------------------------------ gather role, shared lists
-    if (a.dbg & 256) __builtin_amdgcn_s_setprio(2);  // (experiment) gather waves issue first
     const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
     const int s0 = g;
     const bool v0 = s0 < a.nr;
@@ -3009,7 +3009,10 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     }
   } else {
     // ------------------------------------------------------------------ MFMA role
-    if (a.dbg & 512) __builtin_amdgcn_s_setprio(2);  // (experiment) MFMA waves issue first
+    // MFMA waves issue first when both roles are ready (c3 pass 17.0 -> 16.8 ms, repeated A/B in
+    // profiles/r3_ws_prio_ab.log; XPG_WIDE_DBG 512 turns it off): a ready MFMA wave otherwise
+    // waits behind gather waves issuing their address / keep-test VALU work
+    if (!(a.dbg & 512)) __builtin_amdgcn_s_setprio(2);
     const int nb = wave - GW, i32 = lane & 31, h = lane >> 5;
     const bool active = nb * 32 < a.f_out_pad;
     const int col = nb * 32 + i32;
