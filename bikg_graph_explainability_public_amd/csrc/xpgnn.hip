@@ -700,6 +700,7 @@ struct AggArgs {
   int kpitch;
   const uint32_t* mbits;
   const int32_t* f0_node;
+  int rows_blk;  // (diagnostics, XPG_L1_DBG) k_agg_l1_rows: 1 every source kept, 2 every source = the self row
 };
 
 __device__ __forceinline__ float inv_sqrt_deg(float kin) {
@@ -890,9 +891,9 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
         }
         for (int e = e0; e < e1; ++e) {  // uniform
           const int u0 = a.agg_f0[e];
-          const bool keep = kt >= 0.f && (mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
+          const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
           if (keep) {
-            const float* __restrict__ src = T + (int64_t)u0 * W;
+            const float* __restrict__ src = (a.rows_blk & 2) ? selfrow : T + (int64_t)u0 * W;
 #pragma unroll
             for (int f = 0; f < W; ++f) s[f] += src[f];
           }
@@ -907,19 +908,32 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
 #pragma unroll
     for (int f = 0; f < W; ++f) tot[f] += s[f];
   }
-  if (!vrow) return;
-  float4* o = reinterpret_cast<float4*>(a.out + (b * a.n_tgt + t) * a.out_ld);
+  // epilogue: bias + activation, then the 64 rows x W tile leaves through this wave's LDS slice
+  // in 32-float column chunks, so every store instruction writes whole 128-B lines (8 rows x
+  // 128 B).  Stored straight from the lanes (each lane its own 256-B row, 16 B per instruction,
+  // 64 lines per instruction), the lines sat half-written in L2 and HBM saw ~2.4x the bytes.
   const float* bias = a.bias + (a.tgt_type ? (int64_t)a.tgt_type[t] * a.width : 0);
 #pragma unroll
-  for (int j = 0; j < W / 4; ++j) {
-    float v[4];
+  for (int f = 0; f < W; ++f) tot[f] = (f < a.f_real) ? act_apply(tot[f] + bias[f], a.act) : 0.f;
+  __shared__ float l1o[4][64 * 33];
+  float* tile = l1o[threadIdx.x >> 6];
+  const int rr = lane >> 3, q = lane & 7;  // store phase: row rr + 8 i, float4 q of the chunk
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = 4 * j + q;
-      v[q] = (f < a.f_real) ? act_apply(tot[f] + bias[f], a.act) : 0.f;
+  for (int c = 0; c < W / 32; ++c) {
+#pragma unroll
+    for (int f = 0; f < 32; ++f) tile[lane * 33 + f] = tot[32 * c + f];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = rr + 8 * i;
+      const float* src = tile + row * 33 + 4 * q;
+      const float4 v = make_float4(src[0], src[1], src[2], src[3]);
+      if (b0 + row < a.rows)
+        *reinterpret_cast<float4*>(a.out + ((b0 + row) * a.n_tgt + t) * a.out_ld + 32 * c + 4 * q) = v;
     }
-    o[j] = make_float4(v[0], v[1], v[2], v[3]);
+    __builtin_amdgcn_wave_barrier();
   }
+  (void)vrow;
 }
 
 __global__ void k_take_col(const float* __restrict__ C, int64_t M, int64_t ldc, int col,
@@ -4716,8 +4730,11 @@ int launch_agg(const AggArgs& a, hipStream_t st) {
     const int64_t waves = cdiv(a.rows, 64) * a.n_tgt;
     if (waves == 0) return XPG_OK;
     const dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
-    if (a.width == 64) hipLaunchKernelGGL(k_agg_l1_rows<64>, grid, block, 0, st, a);
-    else hipLaunchKernelGGL(k_agg_l1_rows<32>, grid, block, 0, st, a);
+    AggArgs b = a;
+    const char* dg = getenv("XPG_L1_DBG");
+    b.rows_blk = dg ? atoi(dg) : 0;
+    if (a.width == 64) hipLaunchKernelGGL(k_agg_l1_rows<64>, grid, block, 0, st, b);
+    else hipLaunchKernelGGL(k_agg_l1_rows<32>, grid, block, 0, st, b);
     XPG_LAUNCHED();
     return XPG_OK;
   }
