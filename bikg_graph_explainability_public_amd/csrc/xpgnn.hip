@@ -37,6 +37,21 @@ int fail(int code, const std::string& msg) {
 
 #define XPG_LAUNCHED() XPG_HIP(hipGetLastError())
 
+// Diagnostics switches (ablations that change results: XPG_WIDE_DBG, XPG_L1_DBG) are honoured
+// only together with XPG_DIAGNOSTICS=1; set without it they are an error, so a variable leaked
+// into a production environment cannot silently change outputs.
+int diag_env(const char* name, int* out) {
+  const char* v = getenv(name);
+  *out = 0;
+  if (!v || !*v || std::strcmp(v, "0") == 0) return 0;
+  const char* d = getenv("XPG_DIAGNOSTICS");
+  if (!d || std::strcmp(d, "1") != 0)
+    return fail(XPG_EINVAL, std::string(name) + " is a diagnostics switch that changes results: "
+                            "set XPG_DIAGNOSTICS=1 to use it, or unset it");
+  *out = atoi(v);
+  return 0;
+}
+
 #define XPG_REQ(cond, msg)                          \
   do {                                              \
     if (!(cond)) return fail(XPG_EINVAL, (msg));    \
@@ -553,10 +568,12 @@ __global__ void k_shap_approx_rows(const int32_t* __restrict__ cnt, int64_t rows
 }
 
 // pass 2 (one block): the reference's loop `while sum(kernel) == 0 and ref > 0` (kernels.py:
-// 148-162).  Every row value is >= 0 or +inf (M > 0, choose > 0, 0 <= k <= M), so the sum is > 0
-// exactly when some value is > 0: the block scans 1024-row chunks until one holds a positive
-// value (normally the first), instead of summing every row; the ref = int(0.9 ref) back-off
-// recomputes rows in-block.
+// 148-162).  Row values are >= 0, +inf, or negative for an all-active row (k = M + 1, quirk Q5),
+// and a sum holding a NaN or an infinity is != 0: the block scans 1024-row chunks until one
+// holds a value that is not == 0 (normally the first), instead of summing every row (the sum
+// of non-zero values cancelling to exactly 0 is the only case this reads differently, and the
+// reference's own float summation order would decide that case); the ref = int(0.9 ref)
+// back-off recomputes rows in-block.
 __global__ __launch_bounds__(1024) void k_shap_approx_finish(const int32_t* __restrict__ cnt,
                                                              int64_t rows, int64_t cols,
                                                              double* __restrict__ out) {
@@ -566,7 +583,7 @@ __global__ __launch_bounds__(1024) void k_shap_approx_finish(const int32_t* __re
     bool found = false;
     for (int64_t base = 0; base < rows && !found; base += blockDim.x) {  // block-uniform
       const int64_t r = base + threadIdx.x;
-      found = __syncthreads_or(r < rows && out[r] > 0.0) != 0;
+      found = __syncthreads_or(r < rows && !(out[r] == 0.0)) != 0;
     }
     if (found) break;
     ref = static_cast<int>(0.9 * static_cast<double>(ref));
@@ -2422,8 +2439,29 @@ __device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8&
 // the plain gather: bitwise the same A tile.
 constexpr int kIxEdges = 32;                 // listed in-edges per target (32-bit kept masks)
 constexpr int kIxInts = 2 * kIxEdges + 8;    // src[32] | km[32] | b0 b1 tp sm mv + pad
+
+// LFD (lane-feature gather, with IDX): a gather wave owns 4 samples of every target and reads a
+// whole 512-B h1 row per wave-instruction (lane = 2 features, one global_load_dwordx2 off a
+// wave-uniform row address), so a row costs the wave one load + 2 adds and the addresses are
+// scalar work, where the 16-lane groups (one sample each) spent ~95 VALU instructions per sample
+// and target on ballots, slot bookkeeping and 64-bit lane addresses (the SQ counters put the
+// kernel's SIMDs at ~57 % VALU-busy).  The wave's items for a target -- per sample its own row,
+// then its kept listed edges in CSR order -- are issued LF_CAP at a time from a scalar walk;
+// LFD = 1 issues a target's items at the end of the previous interval (as the group gather),
+// LFD = 2 one interval earlier, so a target's rows are in flight for a whole interval (two item
+// sets in registers, every slot loaded -- unused ones from one cached row -- so the compiler's
+// vmcnt counts are exact).  Per sample the rows are summed in the group gather's order: bitwise
+// the same A tile.  Items past LF_CAP (a wave's four samples keeping > ~28 edges) are gathered
+// in place in rounds of 8; targets with in-degree past kIxEdges take a per-sample CSR walk.
+struct LfTgt {  // one target's walk: wave-uniform scalars (no arrays: they stay in SGPRs) and
+                // Mv, lane q = the kept-edge mask of the wave's sample q (read back by v_readlane:
+                // a select chain over four scalars became a private-memory lookup table)
+  int n, b0, b1, tp, sm, ovq, ovself;
+  uint32_t selfm, endm, mv, ovm, Mv;
+};
+
 template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false, int RPF = 4,
-          bool IDX = false>
+          bool IDX = false, int LFD = 0, bool TH = false>
 __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(const WideArgs a) {
   constexpr int RIF = 8;
   // GW / TEAMS = 4 gather waves per target: a group owns samples g and g + 16; 8: sample g
@@ -2498,6 +2536,16 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     }
   };
   const bool ixw = IDX && wave == GW && !(a.dbg & 32);  // the index wave (MFMA wave 0)
+  // TH (with IDX): the layer bias and the head's weight row in LDS after the lists ([f_out_pad]
+  // each), read back four columns at a time by the transposed epilogue
+  float* const HBW = reinterpret_cast<float*>(IX + 3 * kIxInts);
+  if constexpr (TH) {
+    static_assert(IDX && B3 && TEAMS == 1, "transposed head epilogue: B3 IDX kernel");
+    for (int c = tid - 64 * GW; c >= 0 && c < a.f_out_pad; c += 256) {
+      HBW[c] = c < a.f_out ? a.bias[c] : 0.f;
+      HBW[a.f_out_pad + c] = c < a.f_out ? a.H[0].weight[c] : 0.f;
+    }
+  }
   if constexpr (IDX) {
     // prologue: the lists of targets 0 and 1, the chain state of targets 2 (B) and 3 (A)
     if (ixw) {
@@ -2507,7 +2555,267 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     }
     lds_barrier();
   }
-  if (PIPE && IDX && wave < GW) {
+  if (LFD > 0 && wave < GW) {
+    if constexpr (LFD > 0) {
+      // ---------------------------------------------------------------- lane-feature gather role
+      static_assert(PIPE && IDX && B3 && NFI == 8 && GW == 8, "lane-feature gather: IDX lists, B3 tiles, 128-wide rows");
+      constexpr int CAP = LFD == 2 ? 24 : 32;  // items issued per wave and target
+      using bf2 = __bf16 __attribute__((ext_vector_type(2)));
+      // the wave's samples sb .. sb + 3 (readfirstlane: wave-uniform for the compiler too, so the
+      // item walk below is scalar code: SGPR state, scalar branches, saddr loads)
+      const int sb = 4 * __builtin_amdgcn_readfirstlane(wave);
+      const int qv = min(max(a.nr - sb, 0), 4);    // of them, rows of this pass
+      const int kroot = 1 - kagg;                  // host-checked: terms {MEAN, ROOT}
+      __bf16* const Ab = reinterpret_cast<__bf16*>(wsm);
+      const float2* const h1v = reinterpret_cast<const float2*>(a.src);  // row (u, s) = 64 float2
+      const float2* const ctv = reinterpret_cast<const float2*>(a.ctab);
+      const bool run = !(a.dbg & 32);  // dbg 32 (diagnostics): no gathers
+      auto mq = [](const LfTgt& T, int q) -> uint32_t {
+        return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(T.Mv), q));  // q < 64; lanes 4+: 0
+      };
+      // sample q's own row: its h1 row, or the target's inactive-row entry when it masks the target
+      auto self_row = [&](const LfTgt& T, int q) -> const float2* {
+        const int s = sb + q;
+        return (ctv && !((T.mv >> s) & 1u)) ? ctv + (int64_t)T.tp * 64 : h1v + ((int64_t)T.tp * 32 + s) * 64;
+      };
+      // one item of the walk over (sample q, remaining kept edges m, own row pending): its row
+      auto step = [&](const LfTgt& T, int srcv, int& q, uint32_t& m, int& selfp, bool& is_self,
+                      bool& is_end) -> const float2* {
+        const float2* p;
+        if (selfp) {
+          p = self_row(T, q);
+          selfp = 0;
+          is_self = true;
+        } else {
+          const int j = __builtin_ctz(m);
+          m &= m - 1u;
+          p = h1v + ((int64_t)__builtin_amdgcn_readlane(srcv, j) * 32 + sb + q) * 64;
+          is_self = false;
+        }
+        is_end = m == 0u;
+        if (is_end) {
+          ++q;
+          m = mq(T, q);
+          selfp = 1;
+        }
+        q = __builtin_amdgcn_readfirstlane(q);
+        m = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
+        selfp = __builtin_amdgcn_readfirstlane(selfp);
+        return p;
+      };
+      // the MEAN aggregate and the own row of sample q as bf16 hi / lo pieces into the A tile
+      auto finalize = [&](__bf16* A, const LfTgt& T, int q, float2 acc, float2 self, int cnt) {
+        const int s = sb + q;
+        const bool tk = (T.mv >> s) & 1u;
+        const float inv = tk ? 1.f / static_cast<float>(max(cnt + T.sm, 1)) : 0.f;
+        acc.x = fmaf(static_cast<float>(T.sm), self.x, acc.x) * inv;
+        acc.y = fmaf(static_cast<float>(T.sm), self.y, acc.y) * inv;
+        bf2 hi, lo;
+        hi.x = static_cast<__bf16>(acc.x);
+        hi.y = static_cast<__bf16>(acc.y);
+        lo.x = static_cast<__bf16>(acc.x - static_cast<float>(hi.x));
+        lo.y = static_cast<__bf16>(acc.y - static_cast<float>(hi.y));
+        const int ea = s * aph + kagg * a.w_row + 2 * lane;
+        *reinterpret_cast<bf2*>(A + ea) = hi;
+        *reinterpret_cast<bf2*>(A + 32 * aph + ea) = lo;
+        hi.x = static_cast<__bf16>(self.x);
+        hi.y = static_cast<__bf16>(self.y);
+        lo.x = static_cast<__bf16>(self.x - static_cast<float>(hi.x));
+        lo.y = static_cast<__bf16>(self.y - static_cast<float>(hi.y));
+        const int er = s * aph + kroot * a.w_row + 2 * lane;
+        *reinterpret_cast<bf2*>(A + er) = hi;
+        *reinterpret_cast<bf2*>(A + 32 * aph + er) = lo;
+      };
+      // the target's items from the list of target k: a wave-uniform walk, CAP slots
+      auto issue = [&](int k, LfTgt& T, float2 (&r)[CAP]) {
+        T.n = 0;
+        T.selfm = T.endm = T.Mv = 0u;
+        T.b0 = T.b1 = 0;
+        const bool have = k < ntgt_wg;
+        int srcv = 0;
+        if (have) {
+          const int* ix = IX + (k % 3) * kIxInts;
+          T.b0 = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges]);
+          T.b1 = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 1]);
+          T.tp = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 2]);
+          T.sm = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 3]);
+          T.mv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 4]));
+          srcv = lane < kIxEdges ? ix[lane] : 0;
+          const uint32_t kmv = lane < kIxEdges ? static_cast<uint32_t>(ix[kIxEdges + lane]) : 0u;
+          const uint32_t M0 = static_cast<uint32_t>(__ballot((kmv >> sb) & 1u));
+          const uint32_t M1 = static_cast<uint32_t>(__ballot((kmv >> (sb + 1)) & 1u));
+          const uint32_t M2 = static_cast<uint32_t>(__ballot((kmv >> (sb + 2)) & 1u));
+          const uint32_t M3 = static_cast<uint32_t>(__ballot((kmv >> (sb + 3)) & 1u));
+          T.Mv = lane == 0 ? M0 : lane == 1 ? M1 : lane == 2 ? M2 : lane == 3 ? M3 : 0u;
+        }
+        const bool fast = have && T.b1 - T.b0 <= kIxEdges;  // else the CSR walk in consume
+        int q = fast ? 0 : 4, selfp = 1;
+        uint32_t m = fast ? mq(T, 0) : 0u;
+#pragma unroll
+        for (int i = 0; i < CAP; ++i) {
+          const float2* p = h1v;  // unused slot (LFD 2): one cached row
+          const bool it = q < qv;
+          if (it) {
+            bool is_self, is_end;
+            p = step(T, srcv, q, m, selfp, is_self, is_end);
+            T.selfm |= static_cast<uint32_t>(is_self) << i;
+            T.endm |= static_cast<uint32_t>(is_end) << i;
+            T.n = i + 1;
+          }
+          if (LFD == 2 || it) r[i] = p[lane];
+        }
+        T.ovq = q;
+        T.ovm = m;
+        T.ovself = selfp;
+      };
+      // continue the walk in place (items past CAP), 8 rows per round
+      auto inplace = [&](const LfTgt& T, int srcv, int q, uint32_t m, int selfp, float2 acc, float2 self,
+                         __bf16* A) {
+        while (q < qv) {  // wave-uniform
+          float2 rr[8];
+          uint32_t sf = 0u, en = 0u;
+          int nn = 0;
+          const int q0 = q;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (q < qv) {
+              bool is_self, is_end;
+              const float2* p = step(T, srcv, q, m, selfp, is_self, is_end);
+              sf |= static_cast<uint32_t>(is_self) << i;
+              en |= static_cast<uint32_t>(is_end) << i;
+              nn = i + 1;
+              rr[i] = p[lane];
+            }
+          }
+          int qq = q0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (i < nn) {
+              if ((sf >> i) & 1u) {
+                self = rr[i];
+                acc = make_float2(0.f, 0.f);
+              } else {
+                acc.x += rr[i].x;
+                acc.y += rr[i].y;
+              }
+              if ((en >> i) & 1u) {
+                finalize(A, T, qq, acc, self, __popc(mq(T, qq)));
+                ++qq;
+              }
+            }
+          }
+        }
+      };
+      // in-degree past the list: per sample, the CSR from b0 (64 in-edges per chunk), in place
+      auto slow = [&](const LfTgt& T, __bf16* A) {
+        for (int q = 0; q < qv; ++q) {
+          const int s = sb + q;
+          const bool tk = (T.mv >> s) & 1u;
+          const float2 self = self_row(T, q)[lane];
+          float2 acc = make_float2(0.f, 0.f);
+          int cnt = 0;
+          if (tk) {
+            for (int c0 = T.b0; c0 < T.b1; c0 += 64) {
+              const int e = c0 + lane;
+              const int esrc = e < T.b1 ? a.agg_src[e] : 0;
+              const int eu0 = e < T.b1 ? a.agg_f0[e] : 0;
+              const uint32_t em = e < T.b1 ? a.mT0[eu0] : 0u;
+              uint64_t M = __ballot((em >> s) & 1u);
+              cnt += __popcll(M);
+              while (M) {
+                float2 rr[8];
+                int nn = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                  if (M) {
+                    const int j = __builtin_ctzll(M);
+                    M &= M - 1ull;
+                    rr[i] = h1v[((int64_t)__builtin_amdgcn_readlane(esrc, j) * 32 + s) * 64 + lane];
+                    nn = i + 1;
+                  }
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                  if (i < nn) {
+                    acc.x += rr[i].x;
+                    acc.y += rr[i].y;
+                  }
+              }
+            }
+          }
+          finalize(A, T, q, acc, self, cnt);
+        }
+      };
+      auto consume = [&](int k, const LfTgt& T, const float2 (&r)[CAP]) {
+        __bf16* A = Ab + (k & 1) * 2 * abuf;  // abuf floats = 2 abuf bf16
+        if (T.b1 - T.b0 > kIxEdges) {
+          slow(T, A);
+        } else {
+          float2 acc = make_float2(0.f, 0.f), self = make_float2(0.f, 0.f);
+          int qq = 0;
+#pragma unroll
+          for (int i = 0; i < CAP; ++i) {
+            if (i < T.n) {
+              if ((T.selfm >> i) & 1u) {
+                self = r[i];
+                acc = make_float2(0.f, 0.f);
+              } else {
+                acc.x += r[i].x;
+                acc.y += r[i].y;
+              }
+              if ((T.endm >> i) & 1u) {
+                finalize(A, T, qq, acc, self, __popc(mq(T, qq)));
+                ++qq;
+              }
+            }
+          }
+          if (T.ovq < qv) {  // items past CAP (list k is intact until interval k ends)
+            const int srcv = lane < kIxEdges ? IX[(k % 3) * kIxInts + lane] : 0;
+            inplace(T, srcv, T.ovq, T.ovm, T.ovself, acc, self, A);
+          }
+        }
+        for (int q = qv; q < 4; ++q) {  // samples past the pass's rows: zero rows
+          const int s = sb + q;
+          const bf2 z = {static_cast<__bf16>(0.f), static_cast<__bf16>(0.f)};
+          const int ea = s * aph + kagg * a.w_row + 2 * lane, er = s * aph + kroot * a.w_row + 2 * lane;
+          *reinterpret_cast<bf2*>(A + ea) = z;
+          *reinterpret_cast<bf2*>(A + 32 * aph + ea) = z;
+          *reinterpret_cast<bf2*>(A + er) = z;
+          *reinterpret_cast<bf2*>(A + 32 * aph + er) = z;
+        }
+      };
+      if constexpr (LFD == 1) {
+        LfTgt T;
+        float2 r[CAP];
+        if (run) issue(0, T, r);
+        for (int i = 0; i <= nint + 1; ++i) {
+          if (run && i < ntgt_wg) {
+            consume(i, T, r);
+            issue(i + 1, T, r);  // list i + 1: written at interval i - 1 (or the prologue)
+          }
+          lds_barrier();
+        }
+      } else {
+        LfTgt T0, T1;
+        float2 r0[CAP], r1[CAP];
+        if (run) issue(0, T0, r0);
+        for (int i = 0; i <= nint + 1; i += 2) {
+          if (run) {
+            issue(i + 1, T1, r1);  // in flight through interval i + 1's start
+            if (i < ntgt_wg) consume(i, T0, r0);
+          }
+          lds_barrier();
+          if (i + 1 <= nint + 1) {
+            if (run) {
+              issue(i + 2, T0, r0);
+              if (i + 1 < ntgt_wg) consume(i + 1, T1, r1);
+            }
+            lds_barrier();
+          }
+        }
+      }
+    }
+  } else if (PIPE && IDX && wave < GW) {
     // ------------------------------------------------------------------ gather role, shared lists
     const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
     const int s0 = g;
@@ -3107,9 +3415,15 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
             if (kb + 2 < KB) ld(kb + 2, (kb + 2) % 3);
             __builtin_amdgcn_sched_barrier(0);  // keep the reads two k-blocks ahead of their MFMAs
             const int r = kb % 3;
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2[r], whi[kb], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[r], WW[r], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[r], whi[kb], acc, 0, 0, 0);
+            if constexpr (TH) {  // the transposed product: acc[reg] = out[sample i32][column row(reg)]
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(whi[kb], A2[r], acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WW[r], A1[r], acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(whi[kb], A1[r], acc, 0, 0, 0);
+            } else {
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2[r], whi[kb], acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[r], WW[r], acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1[r], whi[kb], acc, 0, 0, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
           }
         } else if constexpr (B3) {
@@ -3168,6 +3482,37 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         }
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
+        if constexpr (TH) {
+          // column c = nb * 32 + (reg & 3) + 8 (reg >> 2) + 4 h of sample i32 sits in acc[reg]:
+          // the head dot over the wave's 32 columns is 16 in-lane FMAs plus one swap of the two
+          // lane halves (the untransposed product needs a 32-lane reduction per register)
+          const float* hb = HBW + nb * 32 + 4 * h;
+          float v = 0.f;
+          if (a.act == XPG_ACT_RELU) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 b4 = *reinterpret_cast<const float4*>(hb + 8 * q);
+              const float4 w4 = *reinterpret_cast<const float4*>(hb + a.f_out_pad + 8 * q);
+              v = fmaf(fmaxf(acc[4 * q] + b4.x, 0.f), w4.x, v);
+              v = fmaf(fmaxf(acc[4 * q + 1] + b4.y, 0.f), w4.y, v);
+              v = fmaf(fmaxf(acc[4 * q + 2] + b4.z, 0.f), w4.z, v);
+              v = fmaf(fmaxf(acc[4 * q + 3] + b4.w, 0.f), w4.w, v);
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float4 b4 = *reinterpret_cast<const float4*>(hb + 8 * q);
+              const float4 w4 = *reinterpret_cast<const float4*>(hb + a.f_out_pad + 8 * q);
+              v = fmaf(act_apply(acc[4 * q] + b4.x, a.act), w4.x, v);
+              v = fmaf(act_apply(acc[4 * q + 1] + b4.y, a.act), w4.y, v);
+              v = fmaf(act_apply(acc[4 * q + 2] + b4.z, a.act), w4.z, v);
+              v = fmaf(act_apply(acc[4 * q + 3] + b4.w, a.act), w4.w, v);
+            }
+          }
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+          v = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);  // both halves: the same sum
+          if (h == 0) H0[slot * a.f_out_pad + nb * 32 + i32] = v;
+        } else {
         float part[16];
         if (a.dbg & 64) {  // dbg 64 (diagnostics): products only, no activation / head reduction
 #pragma unroll
@@ -3191,6 +3536,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
 #pragma unroll
           for (int reg = 0; reg < 16; ++reg) hp[nb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h] = part[reg];
         }
+        }  // !TH
       }
       }
       if (ixw) stC_store(i + 2);  // the list of target i + 2 (read from interval i + 1 on)
@@ -4733,8 +5079,7 @@ int launch_agg(const AggArgs& a, hipStream_t st) {
     if (waves == 0) return XPG_OK;
     const dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
     AggArgs b = a;
-    const char* dg = getenv("XPG_L1_DBG");
-    b.rows_blk = dg ? atoi(dg) : 0;
+    if (const int rc = diag_env("XPG_L1_DBG", &b.rows_blk)) return rc;
     if (a.width == 64) hipLaunchKernelGGL(k_agg_l1_rows<64>, grid, block, 0, st, b);
     else hipLaunchKernelGGL(k_agg_l1_rows<32>, grid, block, 0, st, b);
     XPG_LAUNCHED();
@@ -5032,8 +5377,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   };
   WideArgs a1, a2;
   fill(a1, l1);
-  const char* dbg = getenv("XPG_WIDE_DBG");
-  a1.dbg = dbg ? atoi(dbg) : 0;
+  if (const int rc = diag_env("XPG_WIDE_DBG", &a1.dbg)) return rc;
   a1.n_src = p->n0;
   a1.w_row = l1.f_out_pad;
   a1.rstride = l1.f_out_pad;
@@ -5119,8 +5463,21 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   // (IDX: empty slots cost no loads, default 8: the c3 pass 17.3 -> 17.0 ms over 6)
   const char* rpe = getenv("XPG_WIDE_RP");
   const int rpf = rpe ? atoi(rpe) : idx ? 8 : 6;
+  // lane-feature gather role over the IDX lists (XPG_WIDE_LF: 1 / 2 = items issued one / two
+  // intervals ahead, 0 = the 16-lane group gather)
+  const char* lfe = getenv("XPG_WIDE_LF");
+  const int lfd = idx && lfe ? atoi(lfe) : 0;
+  // transposed MFMA product + in-lane head epilogue (XPG_WIDE_TH=1)
+  const char* the = getenv("XPG_WIDE_TH");
+  const bool th = idx && lfd == 0 && the && std::strcmp(the, "1") == 0;
   if (ws2) {
-    if (pipe && idx) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8, true>
+    if (pipe && idx && lfd == 1) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, 1>;
+    else if (pipe && idx && lfd == 2) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, 2>;
+    else if (pipe && idx && th && rpf == 10) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 10, true, 0, true>;
+    else if (pipe && idx && th) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, 0, true>;
+    else if (pipe && idx && rpf == 12) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 12, true>;
+    else if (pipe && idx && rpf == 10) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 10, true>;
+    else if (pipe && idx) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8, true>
                         : rpf == 6 ? k_wide_last_ws<8, 32, 8, true, 1, true, 6, true>
                                    : k_wide_last_ws<8, 32, 8, true, 1, true, 4, true>;
     else if (pipe) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8>
@@ -5138,7 +5495,8 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const bool l1s_k = k1 == k_wide_l1s<1, true> || k1 == k_wide_l1s<1, false> || k1 == k_wide_l1s<2, true> ||
                      k1 == k_wide_l1s<2, false> || k1 == k_wide_l1s<4, true> || k1 == k_wide_l1s<4, false>;
   if (ws2 && l1s_k && !(cte && std::strcmp(cte, "0") == 0)) a1.ctab = a2.ctab = reinterpret_cast<float*>(ws + W.ct);
-  const size_t lds2 = ws2 ? lds_ws + (idx ? sizeof(int) * 3 * kIxInts : 0) : W.lds;
+  const size_t lds2 = ws2 ? lds_ws + (idx ? sizeof(int) * 3 * kIxInts : 0) + (th ? sizeof(float) * 2 * l2.f_out_pad : 0)
+                          : W.lds;
   const char* gwe0 = getenv("XPG_WIDE_GW");
   const int thr2 = ws2 ? 64 * ((gwe0 && atoi(gwe0) == 4 ? 4 : 8) + 4) : 256;
   const bool l1m = k1 == k_wide_l1m;

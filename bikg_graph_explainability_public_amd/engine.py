@@ -12,6 +12,7 @@ All device memory is owned by torch tensors held by the plan; the C-ABI never al
 """
 import contextlib
 import ctypes
+import os
 import gc
 import math
 
@@ -437,6 +438,7 @@ class ForwardPlan:
         self._layers = (LayerDesc * L)()
         prev_pad = None
         self.terms_kept = []  # per layer: terms after dropping other node types' relations
+        self.lowering = []  # per layer: (kind, relation, destination type) of every kept term
         for li, conv in enumerate(program.convs):
             lvl = li + 1
             n_t = fr[lvl].size
@@ -450,10 +452,11 @@ class ForwardPlan:
                 # destination), so it is dropped — fewer aggregate columns and a shorter K of
                 # the layer's dense product (the query layer of a multi-type plan)
                 tt = np.unique(nt_np[fr[lvl]])
-                if tt.size == 1:
+                if tt.size == 1 and os.environ.get("XPG_PLAN_ALL_TERMS") != "1":  # (A/B switch)
                     kept = [t for t in terms if t.dst_type < 0 or t.dst_type == int(tt[0])]
                     terms = kept or terms
             self.terms_kept.append(len(terms))
+            self.lowering.append(tuple((t.kind, t.rel, t.dst_type) for t in terms))
             ld = self._layers[li]
             ld.n_terms = len(terms)
             ld.act = ACT[conv.act]

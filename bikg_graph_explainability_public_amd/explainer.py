@@ -164,11 +164,14 @@ class Explainer:
     def _verify_key(self, plan, c):
         """What the compiled program's check depends on: the module object, every parameter
         and buffer (storage and in-place version counter: an optimizer step or load_state_dict
-        changes them), the plan kind and the graph's type structure."""
+        changes them), the plan kind, the graph's type structure and the plan's query-dependent
+        lowering (ForwardPlan drops other destination types' relation terms from a layer whose
+        targets share one node type, so two queries can lower the same module differently)."""
         state = tuple((t.data_ptr(), t._version) for t in self.arch.parameters())
         bufs = tuple((t.data_ptr(), t._version) for t in self.arch.buffers())
         return (id(self.arch), state, bufs, self.edge_masks, bool(getattr(plan, "multi_type", False)),
-                tuple(c["h_ntypes"] or ()), tuple(c["h_etypes"] or ()))
+                tuple(c["h_ntypes"] or ()), tuple(c["h_etypes"] or ()),
+                tuple(getattr(plan, "lowering", ())))
 
     # ------------------------------------------------------------------------------ run
     def prepare(self, element, device):
@@ -271,10 +274,11 @@ class Explainer:
         arch_check = "off"
         mode = self.params.get("verify_arch", True)
         if plan is not None and mode:
-            # the check guards the arch lowering (program.compile_arch), which depends on the
-            # module and the graph's type structure, not on the query: once per module state
-            # (parameter storage + in-place version counters) and type structure per Explainer;
-            # params["verify_arch"] = "always" checks every run
+            # the check guards the arch lowering (program.compile_arch + the plan's term
+            # dropping), which depends on the module, the graph's type structure and the query
+            # layer's node types: once per module state (parameter storage + in-place version
+            # counters), type structure and lowering per Explainer; params["verify_arch"] =
+            # "always" checks every run
             key = self._verify_key(plan, c)
             if mode == "always" or key not in self._verified:
                 ok, err = verify()

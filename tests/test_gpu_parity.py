@@ -30,7 +30,8 @@ def _eng():
 
 
 @pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather", "wide-exact",
-                        "wide-teams", "wide-nopipe", "wide-noct", "wide-rp4"])
+                        "wide-teams", "wide-nopipe", "wide-noct", "wide-rp4", "wide-lf1", "wide-lf2",
+                        "wide-th"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
@@ -55,6 +56,10 @@ def fwd_path(request, monkeypatch):
         monkeypatch.setenv("XPG_WIDE_CT", "0")
     if request.param == "wide-rp4":
         monkeypatch.setenv("XPG_WIDE_RP", "4")
+    if request.param in ("wide-lf1", "wide-lf2"):  # lane-feature gather, items 1 / 2 intervals ahead
+        monkeypatch.setenv("XPG_WIDE_LF", request.param[-1])
+    if request.param == "wide-th":  # transposed layer-2 product, in-lane head epilogue
+        monkeypatch.setenv("XPG_WIDE_TH", "1")
     return request.param
 
 
@@ -316,6 +321,25 @@ def test_shap_kernel_vs_reference(cols):
     ref = z[f"c{cols}_kernel"]
     np.testing.assert_allclose(got, ref, rtol=1e-10, atol=0)
     np.testing.assert_array_equal(got == 0, ref == 0)
+
+
+@pytest.mark.parametrize("rows", ["all_active", "all_active_and_empty", "one_empty"])
+def test_shap_kernel_approx_backoff_edge_batches(rows):
+    """The approximate branch's back-off loop (kernels.py:148-162) runs while the kernel SUMS to
+    0: a batch of all-active rows has a negative sum (quirk Q5) and must stop at ref = 1000 like
+    the reference (a test for 'some value > 0' would back off ~60 times and return other values);
+    an empty row is +inf (sum +inf: stop, then cleaned to 0); a lone empty row sums to +inf too."""
+    e = _eng()
+    cols = 1500
+    m = {"all_active": np.ones((5, cols), bool),
+         "all_active_and_empty": np.concatenate([np.ones((3, cols), bool), np.zeros((2, cols), bool)]),
+         "one_empty": np.zeros((1, cols), bool)}[rows]
+    got = e.shap_kernel(e.pack_masks(torch.as_tensor(m).to(DEV)), cols).cpu().numpy()
+    ref = oracle.shap_kernel(m)
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=0)
+    np.testing.assert_array_equal(got == 0, ref == 0)
+    if rows == "all_active":
+        assert (ref < 0).all()
 
 
 def test_kernel_class_seam():
@@ -1017,6 +1041,67 @@ def test_multi_type_engine_vs_oracle_random(hidden, layers):
     m[1] = True
     m[2] = gm.random(S) < 0.05
     _mt_check(c, arch.to(DEV), [m])
+
+
+@pytest.mark.parametrize("hidden", [32, 64])
+def test_layer1_rows_kernel_and_term_dropping_bitwise(hidden, monkeypatch):
+    """The multi-kernel path's layer-1 aggregation with lanes = mask rows (k_agg_l1_rows, the
+    default at widths 32 / 64) against the generic k_agg<true> (XPG_AGG_ROWS=0), bitwise, on a
+    multi-type MEAN + ROOT plan (whose reduced in-degree table makes MEAN sources test their own
+    mask bit) and on a homogeneous GCN plan; and the ForwardPlan lowering that drops the other
+    destination types' relation terms from a single-type layer (the query layer here) against
+    the all-terms plan (XPG_PLAN_ALL_TERMS=1): fewer terms, the same outputs."""
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.nn import ConvStack, HeteroSageStack
+    from golden_utils import multi_type_setup
+    e = _eng()
+    monkeypatch.setenv("XPG_FORWARD", "unfused")
+    monkeypatch.setenv("XPG_FORWARD_STRICT", "1")
+    rels = [("A", "ab", "B"), ("B", "ba", "A"), ("A", "aa", "A"), ("C", "ca", "A"),
+            ("A", "ac", "C")]
+    sizes, dims = {"A": 300, "B": 200, "C": 150}, {"A": 24, "B": 16, "C": 40}
+    g = torch.Generator().manual_seed(hidden)
+    feat = {t: torch.randn(n, dims[t], generator=g).numpy() for t, n in sizes.items()}
+    ei = {r: torch.stack([torch.randint(0, sizes[r[0]], (m,), generator=g),
+                          torch.randint(0, sizes[r[-1]], (m,), generator=g)]).numpy()
+          for r, m in zip(rels, (900, 700, 800, 400, 400))}
+    torch.manual_seed(5)
+    arch = HeteroSageStack(rels, dims, hidden, 2, [hidden, 1]).eval()
+    names = {t: [f"{t.lower()}{i}" for i in range(n)] for t, n in sizes.items()}
+    c = multi_type_setup(feat, ei, names, "b7", "B", 2,
+                         {k: v.numpy() for k, v in arch.state_dict().items()}, [hidden, 1])
+    S = c["x"].shape[0]
+    gm = np.random.default_rng(hidden)
+    m = gm.random((160, S)) < gm.uniform(0.2, 0.9, (160, 1))
+    m[0], m[1] = False, True
+    bits = e.pack_masks(torch.as_tensor(m, device=DEV))
+    plan, _ = _mt_plan(c, arch.to(DEV))
+    monkeypatch.delenv("XPG_AGG_ROWS", raising=False)
+    y_rows = plan.forward(bits)
+    monkeypatch.setenv("XPG_AGG_ROWS", "0")
+    y_gen = plan.forward(bits)
+    monkeypatch.delenv("XPG_AGG_ROWS")
+    assert torch.equal(y_rows, y_gen)
+    monkeypatch.setenv("XPG_PLAN_ALL_TERMS", "1")
+    plan_all, _ = _mt_plan(c, arch)
+    monkeypatch.delenv("XPG_PLAN_ALL_TERMS")
+    assert plan.terms_kept[-1] < plan_all.terms_kept[-1]
+    np.testing.assert_allclose(plan_all.forward(bits).cpu().numpy(), y_rows.cpu().numpy(),
+                               rtol=0, atol=1e-6)
+    # homogeneous GCN (GCN terms: the kept in-degree of every source)
+    n = 400
+    x = torch.randn((n, 16), generator=g)
+    eih = torch.randint(0, n, (2, 2400), generator=g)
+    torch.manual_seed(6)
+    gcn = ConvStack("gcn", [16, hidden, hidden], [hidden, 1]).eval().to(DEV)
+    hp = pipeline.build_plan(gcn, x.to(DEV), eih.to(DEV), [9])
+    mh = gm.random((130, hp.cols)) < 0.6
+    bh = e.pack_masks(torch.as_tensor(mh, device=DEV))
+    monkeypatch.delenv("XPG_AGG_ROWS", raising=False)
+    yh_rows = hp.forward(bh)
+    monkeypatch.setenv("XPG_AGG_ROWS", "0")
+    yh_gen = hp.forward(bh)
+    assert torch.equal(yh_rows, yh_gen)
 
 
 @pytest.mark.parametrize("path", ["engine", "generic"])

@@ -93,6 +93,7 @@ def main():
         rb = args.rows_b
         bits = engine.sample_shapley(13, rb, N, dev)
         for dbg in args.dbg.split(","):
+            os.environ["XPG_DIAGNOSTICS"] = "1"  # XPG_WIDE_DBG is a diagnostics switch
             os.environ["XPG_WIDE_DBG"] = dbg
             ms, y = timed(lambda: plan.forward(bits), reps=2)
             print(f"[B] full forward (XPG_WIDE_DBG={dbg}) {rb} rows x {N} targets: {ms:.3f} ms = "

@@ -2,7 +2,7 @@
 timings of the three forward paths on the c2 bench workload.
 
     XPG_LIB=tools/libxpgnn_stamps.so python tools/fwd_probe.py
-(libxpgnn_stamps.so = xpgnn.hip built with -DXPG_WLM_STAMPS; see scripts/gpu_check.sh)."""
+(libxpgnn_stamps.so = xpgnn.hip built with -DXPG_WLM_STAMPS; see tools/gpu/run.sh)."""
 import ctypes
 import os
 import sys

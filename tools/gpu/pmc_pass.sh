@@ -1,7 +1,7 @@
 #!/bin/bash
 # One rocprofv3 PMC pass per invocation (counters of one block group only), written under
 # gpurun_out/<name>/.  Usage (on the GPU box):
-#   bash scripts/pmc_pass.sh <name> "<counters>" "<kernel regex>" <program args...>
+#   bash tools/gpu/pmc_pass.sh <name> "<counters>" "<kernel regex>" <program args...>
 set -o pipefail
 name=$1; counters=$2; regex=$3; shift 3
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1

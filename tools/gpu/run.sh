@@ -25,6 +25,7 @@ for step in "$@"; do
     # both ranks on cuda:0 (the driver's 8-GPU runs use RCCL, one GPU per rank)
     rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
     capture) run capture 400 python tools/capture_probe.py ;;
+    rank2c4) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2c4 500 python bench.py --gpus 2 --sections c4 --no-cpu-baseline && run rank1c4 300 python bench.py --sections c4 --no-cpu-baseline && grep -h result_checksum gpurun_out/rank2c4.log gpurun_out/rank1c4.log | python -c "import sys, json; [print(json.loads(l)['n_gpus'], json.loads(l)['regimes']['hetero_c4']['result_checksum'], json.loads(l)['regimes']['hetero_c4']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     rank2c5) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2c5 500 python bench.py --gpus 2 --sections c5 --no-cpu-baseline && run rank1c5 300 python bench.py --sections c5 --no-cpu-baseline && grep -h result_checksum gpurun_out/rank2c5.log gpurun_out/rank1c5.log | python -c "import sys, json; [print(json.loads(l)['n_gpus'], json.loads(l)['regimes']['c5_hetero']['result_checksum'], json.loads(l)['regimes']['c5_hetero']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     c5info) run c5info 300 python -u tools/c5_plan_info.py ;;
     c5ab) XPG_AGG_ROWS=0 run c5_aggrows0 300 python bench.py --sections c5 --no-cpu-baseline && run c5_aggrows1 300 python bench.py --sections c5 --no-cpu-baseline && grep -h ms_per_job gpurun_out/c5_aggrows0.log gpurun_out/c5_aggrows1.log | python -c "import sys, json; [print(json.loads(l)['regimes']['c5_hetero']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
@@ -33,7 +34,7 @@ for step in "$@"; do
            run prof_$sec 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$sec -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections $sec ;;
     # layer-2 ablations (c3 full size, one 32-row pass): full, no MFMA, no gathers, no epilogue,
     # exact f32 (B3=0) beside the default bf16x3
-    wsdbg) run wsdbg 500 python tools/ws_ab.py --variants "B3=1;B3=1,DBG=16;B3=1,DBG=32;B3=1,DBG=64;B3=0" ;;
+    wsdbg) XPG_DIAGNOSTICS=1 run wsdbg 500 python tools/ws_ab.py --variants "B3=1;B3=1,DBG=16;B3=1,DBG=32;B3=1,DBG=64;B3=0" ;;
     # FETCH_SIZE / WRITE_SIZE factors per access shape (tools/fetch_calib.hip, known bytes)
     calib) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run calib_fetch 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/calib_fetch -o run -- ./tools/fetch_calib && \
@@ -43,9 +44,15 @@ for step in "$@"; do
     # 2 split poll, 3 both; alternating rounds on one box
     modes) for r in 1 2; do for md in 0 1 2 3; do XPG_MC_MODE=$md run probe_mode${md}_r$r 120 ./tools/wlm_probe 1193 12800 256; done; done ;;
     gw2) run gw2 300 ./tools/gw2_probe ;;
-    wsprof) run wsprof 700 bash scripts/ws_prof.sh ;;
+    # layer-2 SQ counters (two PMC passes of <= 8 SQ counters) on one c3 pass of ws_ab.py
+    wsprof) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run wssq1 300 bash tools/gpu/pmc_pass.sh sq1 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS" "k_wide_l1s|k_wide_last_ws" python3 tools/ws_ab.py --variants "${WSV:-B3=1}" --reps 1 && \
+           run wssq2 300 bash tools/gpu/pmc_pass.sh sq2 "SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES" "k_wide_l1s|k_wide_last_ws" python3 tools/ws_ab.py --variants "${WSV:-B3=1}" --reps 1 ;;
+    # c3 HBM counters per kernel (FETCH_SIZE / WRITE_SIZE passes of the c3 bench section)
+    c3pmc) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run pmc_fetch_c3 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 && \
+           run pmc_write_c3 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 ;;
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
-    wsprof2) run wsprof2 600 bash scripts/ws_prof2.sh ;;
     widetests) run widetests 600 python -u -m pytest tests/test_gpu_coverage.py tests/test_gpu_parity.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wide or c3 or hub" ;;
     idxab) run idxab 600 python -u tools/ws_ab.py --variants "${IDXAB:-B3=1,IDX=0;B3=1;B3=1,IDX=0;B3=1;B3=1,RP=6}" ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;

@@ -4,7 +4,7 @@ import subprocess
 import sys
 
 src = sys.argv[1] if len(sys.argv) > 1 else "bikg_graph_explainability_public_amd/csrc/xpgnn.hip"
-out = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-c", "-o", "/tmp/_kr.o",
+out = subprocess.run(["hipcc", "--offload-arch=gfx950", "--cuda-device-only", "-O3", "-std=c++17", "-fno-slp-vectorize", "-c", "-o", "/tmp/_kr.o",
                       __import__("os").path.abspath(src), "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True,
                      cwd="/tmp").stderr
 cur, rows = None, {}
@@ -21,6 +21,8 @@ filt = sys.argv[2] if len(sys.argv) > 2 else ""
 for name, d in rows.items():
     if filt in name:
         dn = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
-        print(f"{dn[:70]:70s} vgpr={d.get('VGPRs','?'):>4} agpr={d.get('AGPRs','?'):>3} "
+        dn = re.sub(r"\(anonymous namespace\)::", "", dn).replace("void ", "")
+        dn = dn.split("(")[0]
+        print(f"{dn[:80]:80s} vgpr={d.get('VGPRs','?'):>4} agpr={d.get('AGPRs','?'):>3} "
               f"sgpr={d.get('SGPRs','?'):>3} vspill={d.get('VGPRs Spill','?')} "
               f"lds={d.get('LDS Size [bytes/block]','?')} occ={d.get('Occupancy [waves/SIMD]','?')}")

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bikg_graph_explainability_public_amd import _lib, engine, pipeline  # noqa: E402
 from bikg_graph_explainability_public_amd.nn import ConvStack  # noqa: E402
 
-KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW", "DBG", "PIPE", "RP", "CT", "IDX")
+KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW", "DBG", "PIPE", "RP", "CT", "IDX", "LF", "TH")
 
 
 def set_env(spec):
@@ -24,6 +24,10 @@ def set_env(spec):
     for kv in filter(None, spec.split(",")):
         k, v = kv.split("=")
         os.environ["XPG_WIDE_" + k] = v
+    if "DBG=" in spec:  # ablation switches need the diagnostics opt-in
+        os.environ["XPG_DIAGNOSTICS"] = "1"
+    else:
+        os.environ.pop("XPG_DIAGNOSTICS", None)
 
 
 def main():
@@ -60,6 +64,12 @@ def main():
         b.record()
         torch.cuda.synchronize()
         ms = a.elapsed_time(b) / args.reps
+        engine.profile_enable(True)
+        plan.forward(bits)
+        kt = engine.profile_read()
+        engine.profile_enable(False)
+        l1 = kt["wide_l1"][0] / max(1, kt["wide_l1"][1])
+        l2 = kt["wide_l2"][0] / max(1, kt["wide_l2"][1])
         if ref is None:
             set_env("B3=0")
             ref = plan.forward(bits).clone()
@@ -68,8 +78,9 @@ def main():
         if first is None:
             first = y.clone()
         d1 = float((y - first).abs().max())
-        print(f"[{spec:>18s}] {args.rows} rows: {ms:8.3f} ms  max|y - y_exact| = {d:.3e}  "
-              f"max|y - y_first| = {d1:.3e}", flush=True)
+        print(f"[{spec:>18s}] {args.rows} rows: {ms:8.3f} ms  layer1 {l1:7.3f} layer2 {l2:7.3f} ms/pass  "
+              f"max|y - y_exact| = {d:.3e}  max|y - y_first| = {d1:.3e}  bitwise_first={bool(torch.equal(y, first))}",
+              flush=True)
     set_env("")
 
 
