@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/xpgnn.h"
+#include "host_rng.h"
 
 namespace {
 
@@ -5727,6 +5728,16 @@ int launch_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols
 extern "C" {
 
 int xpg_abi_version(void) { return XPG_ABI_VERSION; }
+
+int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t rows, int64_t cols,
+                          uint32_t* bits) {
+  XPG_REQ(state && left && next && (bits || rows == 0) && rows >= 0 && cols > 0, "mt19937_mask_bits: bad arguments");
+  const bool fresh = *left == 1 && *next == 0;  // seeded, not drawn from yet
+  XPG_REQ(fresh || (*left >= 1 && *next >= 0 && *next + *left - 1 == hostrng::kN),
+          "mt19937_mask_bits: generator position (left, next) is not an at::mt19937 state");
+  if (rows > 0) hostrng::mask_bits(state, left, next, rows, cols, bits);
+  return XPG_OK;
+}
 
 #ifdef XPG_WLM_STAMPS  // diagnostic build only: per-phase cycle stamps of the last stamped launch
 int xpg_debug_stamps(uint64_t* out) {

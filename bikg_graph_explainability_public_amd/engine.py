@@ -89,6 +89,32 @@ def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0,
     return bits, counts
 
 
+# torch.get_rng_state() of the CPU generator (at::CPUGeneratorImplState, legacy POD first):
+# uint64 the_initial_seed | int32 left | int32 seeded | uint64 next | uint64 state[624] | ...
+_RNG_LEFT, _RNG_NEXT, _RNG_STATE = 8, 16, 24
+
+
+def compat_shapley_bits(rows: int, cols: int):
+    """torch.randint(0, 2, (rows, cols), dtype=torch.bool) on torch's global CPU generator
+    (masks.py:231-260), bit-identical, as bit-packed int32 [rows, ceil(cols / 32)] rows in host
+    memory (pinned when a GPU is present), with the generator advanced past the draw exactly as
+    torch would advance it: the library replays the generator's MT19937 state natively
+    (xpg_mt19937_mask_bits, host code), without the [rows, cols] bool tensor."""
+    raw = torch.get_rng_state().numpy().copy()
+    left = raw[_RNG_LEFT:_RNG_LEFT + 4].view(np.int32).copy()
+    nxt = np.array([int(raw[_RNG_NEXT:_RNG_NEXT + 8].view(np.uint64)[0])], dtype=np.int32)
+    state = raw[_RNG_STATE:_RNG_STATE + 624 * 8].view(np.uint64).astype(np.uint32)
+    out = torch.empty((rows, words_of(cols)), dtype=torch.int32,
+                      pin_memory=torch.cuda.is_available())
+    call("xpg_mt19937_mask_bits", state.ctypes.data, left.ctypes.data, nxt.ctypes.data, int(rows),
+         int(cols), out.data_ptr() if rows else None)
+    raw[_RNG_LEFT:_RNG_LEFT + 4] = left.view(np.uint8)
+    raw[_RNG_NEXT:_RNG_NEXT + 8] = np.array([nxt[0]], dtype=np.uint64).view(np.uint8)
+    raw[_RNG_STATE:_RNG_STATE + 624 * 8] = state.astype(np.uint64).view(np.uint8)
+    torch.set_rng_state(torch.from_numpy(raw))
+    return out
+
+
 def sample_shapley_dev(seed: torch.Tensor, rows: int, cols: int, row_offset: int = 0,
                        out: torch.Tensor = None):
     """`sample_shapley` with the seed read on the device from `seed` (int64 [1], the bits of a
@@ -389,6 +415,7 @@ class ForwardPlan:
         S = int(sub_feat.shape[0])  # subgraph nodes
         self.n_rel = len(rel_edges)
         self._keep = []  # device tensors referenced by descriptors
+        self._staged = []  # (descriptor, field, int32 array) awaiting the one upload
 
         rel_np = [np.asarray(e.detach().cpu().numpy(), dtype=np.int64).reshape(2, -1)
                   for e in rel_edges]
@@ -417,9 +444,6 @@ class ForwardPlan:
         n0 = fr[0].size
         self.n0 = n0
         self.frontiers = fr
-        self._deg_ptr = self._i32(arr["deg_ptr"])
-        self._deg_src = self._i32(arr["deg_src"] if arr["deg_src"].size else np.zeros(1))
-        self._f0_node = self._i32(fr[0])
 
         X0 = sub_feat.to(device=device, dtype=torch.float32)[torch.as_tensor(fr[0], device=device)]
         f_in0 = program.convs[0].f_in
@@ -465,25 +489,28 @@ class ForwardPlan:
             ld.n_tgt = n_t
             ld.n_edges = int(arr["layers"][li]["agg_src"].size)
             ld.f_in_pad = 0 if li == 0 else prev_pad
-            ld.tgt_prev = self._i32(np.arange(n_t)).data_ptr()  # F_l is a prefix of F_{l-1}
-            ld.tgt_f0 = self._i32(arr["pos"][0][fr[lvl]]).data_ptr()
+            nz = lambda a: a if a.size else np.zeros(1)
+            self._i32(ld, "tgt_prev", np.arange(n_t))  # F_l is a prefix of F_{l-1}
+            self._i32(ld, "tgt_f0", arr["pos"][0][fr[lvl]])
             lay = arr["layers"][li]
-            ld.agg_ptr = self._i32(lay["agg_ptr"]).data_ptr()
-            ld.agg_src = self._i32(lay["agg_src"] if lay["agg_src"].size else np.zeros(1)).data_ptr()
-            ld.agg_f0 = self._i32(lay["agg_f0"] if lay["agg_f0"].size else np.zeros(1)).data_ptr()
-            ld.self_mult = self._i32(lay["self_mult"]).data_ptr()
+            self._i32(ld, "agg_ptr", lay["agg_ptr"])
+            self._i32(ld, "agg_src", nz(lay["agg_src"]))
+            self._i32(ld, "agg_f0", nz(lay["agg_f0"]))
+            self._i32(ld, "self_mult", lay["self_mult"])
             if self.edge_masks:
-                nz = lambda a: a if a.size else np.zeros(1)
-                ld.agg_eid = self._i32(nz(lay["agg_eid"])).data_ptr()
-                ld.self_ptr = self._i32(lay["self_ptr"]).data_ptr()
-                ld.self_eid = self._i32(nz(lay["self_eid"])).data_ptr()
+                self._i32(ld, "agg_eid", nz(lay["agg_eid"]))
+                self._i32(ld, "self_ptr", lay["self_ptr"])
+                self._i32(ld, "self_eid", nz(lay["self_eid"]))
             n_types = program.n_types
             bias = torch.zeros((n_types, f_out_pad), dtype=torch.float32, device=device)
             bias[:, :conv.f_out] = conv.bias.to(device).reshape(-1, conv.f_out)
             self._keep.append(bias)
             ld.bias = bias.data_ptr()
             ld.n_types = n_types
-            ld.tgt_type = self._i32(nt_np[fr[lvl]]).data_ptr() if nt_np is not None else None
+            if nt_np is not None:
+                self._i32(ld, "tgt_type", nt_np[fr[lvl]])
+            else:
+                ld.tgt_type = None
             for k, term in enumerate(terms):
                 ld.terms[k].kind = TERM[term.kind]
                 ld.terms[k].rel = term.rel
@@ -524,15 +551,16 @@ class ForwardPlan:
 
         self.n_out = fr[L].size
         self.desc = ForwardPlanDesc(
-            cols=self.cols, n_rel=self.n_rel, n0=n0, f0_node=self._f0_node.data_ptr(),
-            deg_ptr=self._deg_ptr.data_ptr(), deg_src=self._deg_src.data_ptr(),
+            cols=self.cols, n_rel=self.n_rel, n0=n0,
             n_deg_edges=int(arr["deg_src"].size), n_layers=L,
             layers=self._layers, n_head=len(program.head), head=self._head,
             out_col=program.out_col)
+        self._i32(self.desc, "f0_node", fr[0])
+        self._i32(self.desc, "deg_ptr", arr["deg_ptr"])
+        self._i32(self.desc, "deg_src", arr["deg_src"] if arr["deg_src"].size else np.zeros(1))
         if self.edge_masks:
             self.desc.edge_masks = 1
-            self.desc.deg_eid = self._i32(arr["deg_eid"] if arr["deg_eid"].size
-                                          else np.zeros(1)).data_ptr()
+            self._i32(self.desc, "deg_eid", arr["deg_eid"] if arr["deg_eid"].size else np.zeros(1))
         self.link = link
         if link is not None:
             a, b, act = link
@@ -541,12 +569,28 @@ class ForwardPlan:
             self.desc.edge_dot, self.desc.dot_a, self.desc.dot_b = 1, int(a), int(b)
             self.desc.dot_act = ACT[act]
             self.n_out = 1
+        self._upload_i32()
         self._ws = None
 
-    def _i32(self, a):
-        t = torch.as_tensor(np.ascontiguousarray(a, dtype=np.int32), device=self.device)
-        self._keep.append(t)
-        return t
+    def _i32(self, obj, field, a):
+        """Stage an int32 array for descriptor field `obj.field`; `_upload_i32` moves every
+        staged array to the device in ONE host -> device copy (a plan has ~15-25 of them: one
+        synchronous copy each was ~0.4 ms of Explainer.run) and fills the pointers."""
+        self._staged.append((obj, field, np.ascontiguousarray(a, dtype=np.int32).reshape(-1)))
+
+    def _upload_i32(self):
+        sizes = [(a.size + 15) // 16 * 16 for _, _, a in self._staged]  # 64-B aligned slices
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        host = np.zeros(int(offs[-1]), dtype=np.int32)
+        for (_, _, a), o in zip(self._staged, offs):
+            host[o:o + a.size] = a
+        buf = torch.from_numpy(host).to(self.device)
+        self._keep.append(buf)
+        self.int_arrays = buf  # every staged array, one allocation
+        base = buf.data_ptr()
+        for (obj, field, _), o in zip(self._staged, offs):
+            setattr(obj, field, base + 4 * int(o))
+        self._staged = []
 
     def workspace_bytes(self, rows):
         n = ctypes.c_size_t(0)

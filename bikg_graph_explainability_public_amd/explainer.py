@@ -322,13 +322,12 @@ class Explainer:
                 bits_list.append(engine.sample_communities(seed, cplan, c["sub_pw_inds"], S,
                                                            device, tables=ctabs)[0])
                 masks.append(None)
-            else:
-                mask, _ = Mask(mfeat, sub_ei, c["sub_pw_inds"], self.params,
-                               mproblem).generate()
-                mask = mask.to(device)
-                bits_list.append(engine.pack_masks(mask))
-                masks.append(mask)
-            w0_list.append(LinearRegression(S).layer.weight.detach().reshape(-1))
+            else:  # compat: the reference's CPU draws, bit-identical, packed on the device
+                bits_c, _ = Mask(mfeat, sub_ei, c["sub_pw_inds"], self.params,
+                                 mproblem).generate_bits(device)
+                bits_list.append(bits_c)
+                masks.append(None)
+            w0_list.append(LinearRegression.initial_weights(S))
             dataloader_seed_draw()
         R = bits_list[0].shape[0]
         batch = R // epochs
@@ -475,12 +474,11 @@ class Explainer:
                                  if c["sub_pw_inds"] is None else
                                  engine.sample_communities(seed, cplan, c["sub_pw_inds"], S,
                                                            device, tables=ctabs)[0])
-            else:
-                mask, _ = Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,
-                               self.problem).generate()
-                bits_list.append(engine.pack_masks(mask.to(device)))
+            else:  # compat: the reference's CPU draws, bit-identical, packed on the device
+                bits_list.append(Mask(sub_feat, sub_ei, c["sub_pw_inds"], self.params,
+                                      self.problem).generate_bits(device)[0])
             for q in range(Q):
-                w0[q].append(LinearRegression(S).layer.weight.detach().reshape(-1))
+                w0[q].append(LinearRegression.initial_weights(S))
             dataloader_seed_draw()
         R = bits_list[0].shape[0]
         batch = R // epochs

@@ -165,6 +165,34 @@ class Mask(Data):
             prow = prow[ind]
         return mask, prow
 
+    def generate_bits(self, device):
+        """Compat sampler straight to bit-packed device rows: (bits int32 [R, W], pathway_rows).
+        Community masks: `generate` then packed on the device.  Shapley masks (no communities):
+        the same torch CPU draws replayed natively as packed rows (engine.compat_shapley_bits),
+        then the reference's randperm row shuffle applied on the device -- bit-identical rows
+        and the same generator state afterwards, without the [R, S] bool tensor and its host
+        row gather (masks.py:231-260, 375-380)."""
+        from . import engine
+        if self.pathways is not None:
+            mask, prow = self.generate()
+            if torch.device(device).type == "cpu":  # host callers: the same packing with torch ops
+                R, S = mask.shape
+                W = (S + 31) // 32
+                m = torch.zeros((R, W * 32), dtype=torch.int64)
+                m[:, :S] = mask
+                w = (m.view(R, W, 32) << torch.arange(32, dtype=torch.int64)).sum(-1)
+                return w.to(torch.uint32).view(torch.int32) if hasattr(torch, "uint32") else \
+                    ((w + 2 ** 31) % 2 ** 32 - 2 ** 31).to(torch.int32), prow
+            return engine.pack_masks(mask.to(device)), (prow.to(device) if prow is not None else None)
+        n_perturbs, epochs = self.assertions_mask_generator(self.params)
+        size = torch.Size((n_perturbs * epochs, self.element_count()))  # torch.randint's checks
+        host = engine.compat_shapley_bits(size[0], size[1])
+        ind = torch.randperm(host.shape[0])
+        dev = torch.device(device)
+        if dev.type == "cpu":
+            return host[ind], None
+        return host.to(dev, non_blocking=True)[ind.to(dev)], None
+
     def mask_generator(self):
         """masks.py:262-397 — (DataLoader over the shuffled mask, pathway_rows)."""
         _, epochs = self.assertions_mask_generator(self.params)

@@ -6,6 +6,8 @@ row's GNN output comes from one ForwardPlan launch chain, the KernelSHAP weights
 kernel, and all Adam steps from `xpg_wlm_fit` (one persistent workgroup).  The returned
 weights are the final-epoch weights, as in the reference (quirk Q2, wlm.py:94,264-266).
 """
+import math
+
 import numpy as np
 import torch
 from torch import nn
@@ -26,6 +28,17 @@ class LinearRegression(nn.Module):
 
     def forward(self, X):
         return self.layer(X)
+
+    @staticmethod
+    def initial_weights(num_elements):
+        """The weight row LinearRegression(num_elements) draws, [num_elements]: nn.Linear's
+        reset_parameters (one kaiming_uniform_(a=sqrt(5)) on the [1, S] weight, no bias) on the
+        same torch CPU generator -- bit-identical values and generator state, without building
+        a module per repeat (~35 us each)."""
+        assert isinstance(num_elements, int)
+        w = torch.empty((1, int(num_elements)))
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        return w.reshape(-1)
 
 
 def model_updates(linear_model, loss, best_loss):

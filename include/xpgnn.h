@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 14
+#define XPG_ABI_VERSION 15
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -76,6 +76,14 @@ int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t 
  * the stream (v11). */
 int xpg_sample_shapley_dev(const uint64_t* seed, int64_t row_offset, int64_t rows, int64_t cols,
                            uint32_t* bits, xpg_stream_t stream);
+/* HOST function (no GPU work): the reference's compat Shapley draw torch.randint(0, 2, (rows, cols),
+ * dtype=torch.bool) on torch's CPU generator (masks.py:231-260), replayed from the generator's
+ * at::mt19937 state (state[624] words, left, next as torch.get_rng_state() stores them) and
+ * written as bit-packed rows bits[rows][ceil(cols/32)] (host memory); the state is advanced past
+ * the rows * cols outputs exactly as torch would (the caller writes it back with
+ * torch.set_rng_state).  Bit-identical to the torch draw (v15). */
+int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t rows, int64_t cols,
+                          uint32_t* bits);
 /* Same bits, plus counts[r] = popcount of row r (the KernelSHAP coalition sizes, kernels.py:144),
  * accumulated while sampling so KernelSHAP needs no second pass over the bits. */
 int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,

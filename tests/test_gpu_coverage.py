@@ -15,6 +15,7 @@
 Reference semantics cited: data.py:331 / model.py:62-116 (no degree limit), masks.py:262-397,
 pathways.py:387-429, explainer.py:490-532, wlm.py:132-278.
 """
+import contextlib
 import os
 import socket
 import sys
@@ -86,6 +87,21 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_TH", "1")
     else:
         monkeypatch.delenv("XPG_WIDE_TH", raising=False)
+
+
+@contextlib.contextmanager
+def _env(**kv):
+    """Set XPG_* switches for the block, restoring the previous values."""
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update(kv)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _spec(kind, dims, fc, arch):
@@ -236,6 +252,17 @@ def test_c3_full_graph_sampled_columns():
     # all-off row: no edge survives anywhere, so every output is the node's isolated value
     iso = oracle.forward_union(spec, xn[cols], {None: (np.zeros(0, np.int64),) * 2})[:, 0]
     np.testing.assert_allclose(ysel[1, cols], iso, rtol=0, atol=1e-5)
+    # every output of the first pass (32 rows x all 1M targets) of the default three-piece bf16
+    # layer 2 (and its transposed-head / lane-feature variants) against the exact-f32 MFMA
+    # kernel (XPG_WIDE_B3=0): the split-precision error bound over whole rows, not 48 columns
+    b32 = bits[:32].contiguous()
+    with _env(XPG_WIDE_B3="0"):
+        y_ex = plan.forward(b32)
+    for variant in ({}, {"XPG_WIDE_TH": "1"}, {"XPG_WIDE_LF": "2"}):
+        with _env(**variant):
+            y_v = plan.forward(b32)
+        d = float((y_v - y_ex).abs().max())
+        assert d <= 1e-5, f"{variant or 'default'}: max |y - y_exact| = {d:.3g} over 32 x {N}"
 
 
 # ------------------------------------------------------------------ reduced c5
@@ -314,6 +341,144 @@ def test_c5_shaped_explainer_vs_oracle():
     assert pdf is not None and len(pdf) == len(ref) >= 15  # communities meeting the subgraph
     np.testing.assert_allclose(pdf.reindex([n for n, _ in ref])["score"].values,
                                [s for _, s in ref], rtol=0, atol=1e-4)
+
+
+# ------------------------------------------------------------------ c5 / c4 at configured size
+def _hetero_full_check(exp, lr, feat, ei, names, element, element_type, n_layers, arch, fc,
+                       q4, rows_per_repeat=64, pathways=None, pw_names=None, df=None, pdf=None,
+                       params=None):
+    """Oracle checks of a full-size multi-type Explainer.run (every repeat): per-copy outputs of
+    `rows_per_repeat` sampled rows through the run's own plan (plus, with Q4, every batch's
+    surviving copy = the targets the fit used), KernelSHAP of every row, every fit, the mean /
+    std DataFrame and the community scores."""
+    from golden_utils import multi_type_setup
+    e = _eng()
+    c = multi_type_setup({k: v.numpy() for k, v in feat.items()}, {k: v.numpy() for k, v in ei.items()},
+                         names, element, element_type, n_layers,
+                         {k: v.cpu().numpy() for k, v in arch.state_dict().items()}, fc)
+    S = c["x"].shape[0]
+    assert lr["S"] == S
+    plan = lr["plan"]
+    rng = np.random.default_rng(0)
+    ws = []
+    for i, rp in enumerate(lr["repeats"]):
+        bits = rp["bits"]
+        R, B = bits.shape[0], rp["batch"]
+        m_all = e.unpack_masks(bits, S).cpu().numpy()
+        sel = np.sort(rng.choice(R, rows_per_repeat, replace=False))
+        if q4:  # the surviving copy of every batch (row r0 + sub_ind) is the batch's target
+            sel = np.union1d(sel, np.arange(c["sub_ind"], R, B))
+        selt = torch.as_tensor(sel, device=DEV)
+        y_sel = plan.forward(bits[selt].contiguous())[:, 0]
+        copy = oracle.hetero_multi_copy_outputs(c["spec"], c["x"], c["nt"], c["ei"], c["et"],
+                                                c["ntypes"], c["rels"], c["pads"], m_all[sel],
+                                                c["sub_ind"])
+        nonempty = copy != 0
+        np.testing.assert_allclose(y_sel.cpu().numpy()[nonempty], copy[nonempty], rtol=0, atol=1e-5,
+                                   err_msg=f"repeat {i} copy outputs")
+        yt = rp["y"].cpu().numpy()
+        if q4:
+            for b0 in range(0, R, B):
+                j = int(np.searchsorted(sel, b0 + c["sub_ind"]))
+                np.testing.assert_allclose(yt[b0:b0 + B], copy[j], rtol=0, atol=1e-5)
+        else:
+            np.testing.assert_allclose(yt[sel], copy, rtol=0, atol=1e-5, err_msg=f"repeat {i} targets")
+        k = oracle.shap_kernel(m_all)
+        np.testing.assert_allclose(rp["kernel"].cpu().numpy(), k, rtol=1e-10, atol=0)
+        w, _, best = oracle.train_wlm(m_all, B, yt, k, rp["w0"].cpu().numpy(), params)
+        np.testing.assert_allclose(lr["weights"][i].cpu().numpy(), w, rtol=0, atol=1e-4)
+        assert int(rp["best_epoch"]) == best
+        ws.append(w)
+    mean, std = oracle.weight_stacking(ws)
+    got = df.reindex(c["sub_names"])
+    np.testing.assert_allclose(got["config_value_mean"].values, mean, rtol=0, atol=1e-4)
+    np.testing.assert_allclose(got["config_value_std"].values, std, rtol=0, atol=1e-4)
+    if pathways is not None:
+        sub_pw, sub_pw_names = oracle.pathways_comp_graph(pathways, pw_names, c["sub_names"])
+        ref = oracle.aggregate(mean.astype(np.float32), oracle.names2inds(sub_pw, c["sub_names"]),
+                               sub_pw_names)
+        assert pdf is not None and len(pdf) == len(ref)
+        np.testing.assert_allclose(pdf.reindex([n for n, _ in ref])["score"].values,
+                                   [sc for _, sc in ref], rtol=0, atol=1e-4)
+    return S
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_size_explainer_vs_oracle():
+    """BASELINE configs[4] at its configured size through the public API: a 1M-node 3-type graph
+    (500k gene / 300k protein / 200k drug, 256-dim features, 5 relations x 2M edges),
+    2-layer HeteroConv(SAGE) 256 -> 64 -> 64 + head 64 -> 16 -> 1, node_prediction of gene 7,
+    20 communities over the whole graph (filtered to the subgraph as the reference filters
+    them), the device community sampler, interpret_samples = 1024 x epochs = 50, 2 repeats,
+    the reference's Q4 targets.  The kernels this runs at full size (k_agg_l1_rows at width 64,
+    the column-mask community sampler, the dropped-term query layer, xpg_rows_no_edge) are
+    checked against the oracle on the full subgraph (model.py:118-253, wlm.py:435-436,
+    pathways.py:387-429)."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    from bikg_graph_explainability_public_amd.nn import HeteroSageStack
+    sizes = {"gene": 500_000, "protein": 300_000, "drug": 200_000}
+    F = 256
+    g = torch.Generator().manual_seed(5)
+    feat = {t: torch.randn((n, F), generator=g) for t, n in sizes.items()}
+    rels = [("gene", "gp", "protein"), ("protein", "pg", "gene"), ("gene", "gg", "gene"),
+            ("drug", "dg", "gene"), ("gene", "gd", "drug")]
+    ei = {r: torch.stack([torch.randint(0, sizes[r[0]], (2_000_000,), generator=g),
+                          torch.randint(0, sizes[r[-1]], (2_000_000,), generator=g)]) for r in rels}
+    torch.manual_seed(0)
+    fc = [64, 16, 1]
+    arch = HeteroSageStack(rels, {t: F for t in sizes}, 64, 2, fc).eval()
+    names = {t: [f"{t}{i}" for i in range(n)] for t, n in sizes.items()}
+    all_names = [n for t in sizes for n in names[t]]
+    rng = np.random.default_rng(20)
+    perm = rng.permutation(len(all_names))
+    cuts = np.sort(rng.choice(np.arange(1, len(all_names)), 19, replace=False))
+    pathways = [[all_names[i] for i in c] for c in np.split(perm, cuts)]
+    pw_names = [f"P{i}" for i in range(20)]
+    params = {"seed": 3, "interpret_samples": 1024, "epochs": 50, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": "device"}
+    exp = Explainer({k: v.to(DEV) for k, v in feat.items()}, {k: v.to(DEV) for k, v in ei.items()},
+                    arch.to(DEV), params, names, pathways, pw_names, "gene", problem="node_prediction")
+    torch.manual_seed(99)
+    df, pdf = exp.run("gene7", 2)
+    lr = exp.last_run
+    assert lr["engine"] and len(lr["repeats"]) == 2
+    S = _hetero_full_check(exp, lr, feat, ei, names, "gene7", "gene", 2, arch, fc, q4=True,
+                           pathways=pathways, pw_names=pw_names, df=df, pdf=pdf, params=params)
+    assert S > 1000  # the configured workload's subgraph (~1.4k nodes), not a toy
+
+
+@pytest.mark.timeout(900)
+def test_c4_full_size_explainer_vs_oracle():
+    """BASELINE configs[3] at its configured size through the public API: 500k nodes in 3 types
+    (200k gene / 200k protein / 100k drug, 84 / 64 / 32 features), 5 relations x 1M edges,
+    one HeteroConv(SAGE) layer 84 -> 16 + head 16 -> 16 -> 32 -> 1 (the gcn_hetero_1hop shape),
+    node_prediction of gene 7, Shapley device sampler, interpret_samples = 256 x epochs = 50,
+    2 repeats, per-copy targets (hetero_q4=False: the reference's Q4 extraction cannot run at
+    this shape, batch > subgraph)."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    from bikg_graph_explainability_public_amd.nn import HeteroSageStack
+    sizes = {"gene": 200_000, "protein": 200_000, "drug": 100_000}
+    dims = {"gene": 84, "protein": 64, "drug": 32}
+    g = torch.Generator().manual_seed(4)
+    feat = {t: torch.randn((n, dims[t]), generator=g) for t, n in sizes.items()}
+    rels = [("gene", "gp", "protein"), ("protein", "pg", "gene"), ("gene", "gg", "gene"),
+            ("drug", "dg", "gene"), ("gene", "gd", "drug")]
+    ei = {r: torch.stack([torch.randint(0, sizes[r[0]], (1_000_000,), generator=g),
+                          torch.randint(0, sizes[r[-1]], (1_000_000,), generator=g)]) for r in rels}
+    torch.manual_seed(0)
+    fc = [16, 16, 32, 1]
+    arch = HeteroSageStack(rels, dims, 16, 1, fc).eval()
+    names = {t: [f"{t}{i}" for i in range(n)] for t, n in sizes.items()}
+    params = {"seed": 3, "interpret_samples": 256, "epochs": 50, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": "device", "hetero_q4": False}
+    exp = Explainer({k: v.to(DEV) for k, v in feat.items()}, {k: v.to(DEV) for k, v in ei.items()},
+                    arch.to(DEV), params, names, None, None, "gene", problem="node_prediction")
+    torch.manual_seed(98)
+    df, _ = exp.run("gene7", 2)
+    lr = exp.last_run
+    assert lr["engine"] and len(lr["repeats"]) == 2
+    _hetero_full_check(exp, lr, feat, ei, names, "gene7", "gene", 1, arch, fc, q4=False, df=df,
+                       params=params)
 
 
 # ------------------------------------------------------------------ fit failure is loud
@@ -469,19 +634,22 @@ def test_explainer_arch_check_keyed_on_query_lowering():
     reuses it, and every result equals a fresh Explainer's."""
     from bikg_graph_explainability_public_amd.explainer import Explainer
     from bikg_graph_explainability_public_amd.nn import HeteroSageStack
-    rels = [("A", "ab", "B"), ("B", "ba", "A"), ("A", "aa", "A"), ("B", "bb", "B"),
-            ("A", "ac", "C")]  # 5 MEAN + 3 ROOT terms per conv (the engine takes <= 8)
+    # every type a destination (a 2-layer HeteroConv needs each source type's layer-1 output):
+    # 5 MEAN + 3 ROOT terms per conv (the engine takes <= 8)
+    rels = [("A", "ab", "B"), ("B", "ba", "A"), ("B", "bb", "B"), ("C", "ca", "A"), ("A", "ac", "C")]
     sizes, dims = {"A": 60, "B": 40, "C": 30}, {"A": 8, "B": 6, "C": 10}
     g = torch.Generator().manual_seed(5)
     feat = {t: torch.randn(n, dims[t], generator=g) for t, n in sizes.items()}
     ei = {}
-    for r, m in zip(rels, (200, 150, 200, 120, 100)):
+    for r, m in zip(rels, (200, 150, 120, 100, 100)):
         e = torch.stack([torch.randint(0, sizes[r[0]], (m,), generator=g),
                          torch.randint(0, sizes[r[-1]], (m,), generator=g)])
         if r[1] == "ab":  # b1, b2: in-neighbours of type B only; b0: an A in-neighbour
-            e = torch.cat([e[:, (e[1] != 1) & (e[1] != 2)], torch.tensor([[3], [0]])], 1)
-        if r[1] == "bb":
+            e = torch.cat([e[:, (e[1] != 1) & (e[1] != 2)], torch.tensor([[3, 5, 5, 5], [0, 5, 7, 9]])], 1)
+        if r[1] == "bb":  # every type within 3 hops of b0 / b1 / b2 (the generic check needs all)
             e = torch.cat([e, torch.tensor([[5, 7, 9], [0, 1, 2]])], 1)
+        if r[1] == "ca":
+            e = torch.cat([e, torch.tensor([[0, 0], [5, 3]])], 1)
         ei[r] = e
     torch.manual_seed(3)
     arch = HeteroSageStack(rels, dims, 16, 2, [16, 1]).eval()
