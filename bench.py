@@ -762,8 +762,8 @@ C3_KERNELS = ("k_wide_bits", "k_wide_f0", "k_wide_degree", "k_wide_l1s", "k_wide
 # defaults), as rocprofv3 names them: the counter bytes of the line are these kernels' own
 # dispatches (the exact-f32 comparison pass is another instantiation and is not mixed in)
 C3_DEFAULT_INSTANCES = {"k_wide_l1s": "k_wide_l1s<2, false>",
-                        "k_wide_last_ws": "k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, 0, false>"}
-C3_EXACT_F32_INSTANCE = "k_wide_last_ws<8, 32, 8, false, 1, false, 4, false, 0, false>"
+                        "k_wide_last_ws": "k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, true>"}
+C3_EXACT_F32_INSTANCE = "k_wide_last_ws<8, 32, 8, false, 1, false, 4, false, false>"
 
 
 def c3_section(args, dev, world, rank):

@@ -2441,28 +2441,9 @@ __device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8&
 constexpr int kIxEdges = 32;                 // listed in-edges per target (32-bit kept masks)
 constexpr int kIxInts = 2 * kIxEdges + 8;    // src[32] | km[32] | b0 b1 tp sm mv + pad
 
-// LFD (lane-feature gather, with IDX): a gather wave owns 4 samples of every target and reads a
-// whole 512-B h1 row per wave-instruction (lane = 2 features, one global_load_dwordx2 off a
-// wave-uniform row address), so a row costs the wave one load + 2 adds and the addresses are
-// scalar work, where the 16-lane groups (one sample each) spent ~95 VALU instructions per sample
-// and target on ballots, slot bookkeeping and 64-bit lane addresses (the SQ counters put the
-// kernel's SIMDs at ~57 % VALU-busy).  The wave's items for a target -- per sample its own row,
-// then its kept listed edges in CSR order -- are issued LF_CAP at a time from a scalar walk;
-// LFD = 1 issues a target's items at the end of the previous interval (as the group gather),
-// LFD = 2 one interval earlier, so a target's rows are in flight for a whole interval (two item
-// sets in registers, every slot loaded -- unused ones from one cached row -- so the compiler's
-// vmcnt counts are exact).  Per sample the rows are summed in the group gather's order: bitwise
-// the same A tile.  Items past LF_CAP (a wave's four samples keeping > ~28 edges) are gathered
-// in place in rounds of 8; targets with in-degree past kIxEdges take a per-sample CSR walk.
-struct LfTgt {  // one target's walk: wave-uniform scalars (no arrays: they stay in SGPRs) and
-                // Mv, lane q = the kept-edge mask of the wave's sample q (read back by v_readlane:
-                // a select chain over four scalars became a private-memory lookup table)
-  int n, b0, b1, tp, sm, ovq, ovself;
-  uint32_t selfm, endm, mv, ovm, Mv;
-};
 
 template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false, int RPF = 4,
-          bool IDX = false, int LFD = 0, bool TH = false>
+          bool IDX = false, bool TH = false>
 __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(const WideArgs a) {
   constexpr int RIF = 8;
   // GW / TEAMS = 4 gather waves per target: a group owns samples g and g + 16; 8: sample g
@@ -2556,267 +2537,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     }
     lds_barrier();
   }
-  if (LFD > 0 && wave < GW) {
-    if constexpr (LFD > 0) {
-      // ---------------------------------------------------------------- lane-feature gather role
-      static_assert(PIPE && IDX && B3 && NFI == 8 && GW == 8, "lane-feature gather: IDX lists, B3 tiles, 128-wide rows");
-      constexpr int CAP = LFD == 2 ? 24 : 32;  // items issued per wave and target
-      using bf2 = __bf16 __attribute__((ext_vector_type(2)));
-      // the wave's samples sb .. sb + 3 (readfirstlane: wave-uniform for the compiler too, so the
-      // item walk below is scalar code: SGPR state, scalar branches, saddr loads)
-      const int sb = 4 * __builtin_amdgcn_readfirstlane(wave);
-      const int qv = min(max(a.nr - sb, 0), 4);    // of them, rows of this pass
-      const int kroot = 1 - kagg;                  // host-checked: terms {MEAN, ROOT}
-      __bf16* const Ab = reinterpret_cast<__bf16*>(wsm);
-      const float2* const h1v = reinterpret_cast<const float2*>(a.src);  // row (u, s) = 64 float2
-      const float2* const ctv = reinterpret_cast<const float2*>(a.ctab);
-      const bool run = !(a.dbg & 32);  // dbg 32 (diagnostics): no gathers
-      auto mq = [](const LfTgt& T, int q) -> uint32_t {
-        return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(T.Mv), q));  // q < 64; lanes 4+: 0
-      };
-      // sample q's own row: its h1 row, or the target's inactive-row entry when it masks the target
-      auto self_row = [&](const LfTgt& T, int q) -> const float2* {
-        const int s = sb + q;
-        return (ctv && !((T.mv >> s) & 1u)) ? ctv + (int64_t)T.tp * 64 : h1v + ((int64_t)T.tp * 32 + s) * 64;
-      };
-      // one item of the walk over (sample q, remaining kept edges m, own row pending): its row
-      auto step = [&](const LfTgt& T, int srcv, int& q, uint32_t& m, int& selfp, bool& is_self,
-                      bool& is_end) -> const float2* {
-        const float2* p;
-        if (selfp) {
-          p = self_row(T, q);
-          selfp = 0;
-          is_self = true;
-        } else {
-          const int j = __builtin_ctz(m);
-          m &= m - 1u;
-          p = h1v + ((int64_t)__builtin_amdgcn_readlane(srcv, j) * 32 + sb + q) * 64;
-          is_self = false;
-        }
-        is_end = m == 0u;
-        if (is_end) {
-          ++q;
-          m = mq(T, q);
-          selfp = 1;
-        }
-        q = __builtin_amdgcn_readfirstlane(q);
-        m = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(m)));
-        selfp = __builtin_amdgcn_readfirstlane(selfp);
-        return p;
-      };
-      // the MEAN aggregate and the own row of sample q as bf16 hi / lo pieces into the A tile
-      auto finalize = [&](__bf16* A, const LfTgt& T, int q, float2 acc, float2 self, int cnt) {
-        const int s = sb + q;
-        const bool tk = (T.mv >> s) & 1u;
-        const float inv = tk ? 1.f / static_cast<float>(max(cnt + T.sm, 1)) : 0.f;
-        acc.x = fmaf(static_cast<float>(T.sm), self.x, acc.x) * inv;
-        acc.y = fmaf(static_cast<float>(T.sm), self.y, acc.y) * inv;
-        bf2 hi, lo;
-        hi.x = static_cast<__bf16>(acc.x);
-        hi.y = static_cast<__bf16>(acc.y);
-        lo.x = static_cast<__bf16>(acc.x - static_cast<float>(hi.x));
-        lo.y = static_cast<__bf16>(acc.y - static_cast<float>(hi.y));
-        const int ea = s * aph + kagg * a.w_row + 2 * lane;
-        *reinterpret_cast<bf2*>(A + ea) = hi;
-        *reinterpret_cast<bf2*>(A + 32 * aph + ea) = lo;
-        hi.x = static_cast<__bf16>(self.x);
-        hi.y = static_cast<__bf16>(self.y);
-        lo.x = static_cast<__bf16>(self.x - static_cast<float>(hi.x));
-        lo.y = static_cast<__bf16>(self.y - static_cast<float>(hi.y));
-        const int er = s * aph + kroot * a.w_row + 2 * lane;
-        *reinterpret_cast<bf2*>(A + er) = hi;
-        *reinterpret_cast<bf2*>(A + 32 * aph + er) = lo;
-      };
-      // the target's items from the list of target k: a wave-uniform walk, CAP slots
-      auto issue = [&](int k, LfTgt& T, float2 (&r)[CAP]) {
-        T.n = 0;
-        T.selfm = T.endm = T.Mv = 0u;
-        T.b0 = T.b1 = 0;
-        const bool have = k < ntgt_wg;
-        int srcv = 0;
-        if (have) {
-          const int* ix = IX + (k % 3) * kIxInts;
-          T.b0 = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges]);
-          T.b1 = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 1]);
-          T.tp = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 2]);
-          T.sm = __builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 3]);
-          T.mv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(ix[2 * kIxEdges + 4]));
-          srcv = lane < kIxEdges ? ix[lane] : 0;
-          const uint32_t kmv = lane < kIxEdges ? static_cast<uint32_t>(ix[kIxEdges + lane]) : 0u;
-          const uint32_t M0 = static_cast<uint32_t>(__ballot((kmv >> sb) & 1u));
-          const uint32_t M1 = static_cast<uint32_t>(__ballot((kmv >> (sb + 1)) & 1u));
-          const uint32_t M2 = static_cast<uint32_t>(__ballot((kmv >> (sb + 2)) & 1u));
-          const uint32_t M3 = static_cast<uint32_t>(__ballot((kmv >> (sb + 3)) & 1u));
-          T.Mv = lane == 0 ? M0 : lane == 1 ? M1 : lane == 2 ? M2 : lane == 3 ? M3 : 0u;
-        }
-        const bool fast = have && T.b1 - T.b0 <= kIxEdges;  // else the CSR walk in consume
-        int q = fast ? 0 : 4, selfp = 1;
-        uint32_t m = fast ? mq(T, 0) : 0u;
-#pragma unroll
-        for (int i = 0; i < CAP; ++i) {
-          const float2* p = h1v;  // unused slot (LFD 2): one cached row
-          const bool it = q < qv;
-          if (it) {
-            bool is_self, is_end;
-            p = step(T, srcv, q, m, selfp, is_self, is_end);
-            T.selfm |= static_cast<uint32_t>(is_self) << i;
-            T.endm |= static_cast<uint32_t>(is_end) << i;
-            T.n = i + 1;
-          }
-          if (LFD == 2 || it) r[i] = p[lane];
-        }
-        T.ovq = q;
-        T.ovm = m;
-        T.ovself = selfp;
-      };
-      // continue the walk in place (items past CAP), 8 rows per round
-      auto inplace = [&](const LfTgt& T, int srcv, int q, uint32_t m, int selfp, float2 acc, float2 self,
-                         __bf16* A) {
-        while (q < qv) {  // wave-uniform
-          float2 rr[8];
-          uint32_t sf = 0u, en = 0u;
-          int nn = 0;
-          const int q0 = q;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (q < qv) {
-              bool is_self, is_end;
-              const float2* p = step(T, srcv, q, m, selfp, is_self, is_end);
-              sf |= static_cast<uint32_t>(is_self) << i;
-              en |= static_cast<uint32_t>(is_end) << i;
-              nn = i + 1;
-              rr[i] = p[lane];
-            }
-          }
-          int qq = q0;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            if (i < nn) {
-              if ((sf >> i) & 1u) {
-                self = rr[i];
-                acc = make_float2(0.f, 0.f);
-              } else {
-                acc.x += rr[i].x;
-                acc.y += rr[i].y;
-              }
-              if ((en >> i) & 1u) {
-                finalize(A, T, qq, acc, self, __popc(mq(T, qq)));
-                ++qq;
-              }
-            }
-          }
-        }
-      };
-      // in-degree past the list: per sample, the CSR from b0 (64 in-edges per chunk), in place
-      auto slow = [&](const LfTgt& T, __bf16* A) {
-        for (int q = 0; q < qv; ++q) {
-          const int s = sb + q;
-          const bool tk = (T.mv >> s) & 1u;
-          const float2 self = self_row(T, q)[lane];
-          float2 acc = make_float2(0.f, 0.f);
-          int cnt = 0;
-          if (tk) {
-            for (int c0 = T.b0; c0 < T.b1; c0 += 64) {
-              const int e = c0 + lane;
-              const int esrc = e < T.b1 ? a.agg_src[e] : 0;
-              const int eu0 = e < T.b1 ? a.agg_f0[e] : 0;
-              const uint32_t em = e < T.b1 ? a.mT0[eu0] : 0u;
-              uint64_t M = __ballot((em >> s) & 1u);
-              cnt += __popcll(M);
-              while (M) {
-                float2 rr[8];
-                int nn = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                  if (M) {
-                    const int j = __builtin_ctzll(M);
-                    M &= M - 1ull;
-                    rr[i] = h1v[((int64_t)__builtin_amdgcn_readlane(esrc, j) * 32 + s) * 64 + lane];
-                    nn = i + 1;
-                  }
-                }
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                  if (i < nn) {
-                    acc.x += rr[i].x;
-                    acc.y += rr[i].y;
-                  }
-              }
-            }
-          }
-          finalize(A, T, q, acc, self, cnt);
-        }
-      };
-      auto consume = [&](int k, const LfTgt& T, const float2 (&r)[CAP]) {
-        __bf16* A = Ab + (k & 1) * 2 * abuf;  // abuf floats = 2 abuf bf16
-        if (T.b1 - T.b0 > kIxEdges) {
-          slow(T, A);
-        } else {
-          float2 acc = make_float2(0.f, 0.f), self = make_float2(0.f, 0.f);
-          int qq = 0;
-#pragma unroll
-          for (int i = 0; i < CAP; ++i) {
-            if (i < T.n) {
-              if ((T.selfm >> i) & 1u) {
-                self = r[i];
-                acc = make_float2(0.f, 0.f);
-              } else {
-                acc.x += r[i].x;
-                acc.y += r[i].y;
-              }
-              if ((T.endm >> i) & 1u) {
-                finalize(A, T, qq, acc, self, __popc(mq(T, qq)));
-                ++qq;
-              }
-            }
-          }
-          if (T.ovq < qv) {  // items past CAP (list k is intact until interval k ends)
-            const int srcv = lane < kIxEdges ? IX[(k % 3) * kIxInts + lane] : 0;
-            inplace(T, srcv, T.ovq, T.ovm, T.ovself, acc, self, A);
-          }
-        }
-        for (int q = qv; q < 4; ++q) {  // samples past the pass's rows: zero rows
-          const int s = sb + q;
-          const bf2 z = {static_cast<__bf16>(0.f), static_cast<__bf16>(0.f)};
-          const int ea = s * aph + kagg * a.w_row + 2 * lane, er = s * aph + kroot * a.w_row + 2 * lane;
-          *reinterpret_cast<bf2*>(A + ea) = z;
-          *reinterpret_cast<bf2*>(A + 32 * aph + ea) = z;
-          *reinterpret_cast<bf2*>(A + er) = z;
-          *reinterpret_cast<bf2*>(A + 32 * aph + er) = z;
-        }
-      };
-      if constexpr (LFD == 1) {
-        LfTgt T;
-        float2 r[CAP];
-        if (run) issue(0, T, r);
-        for (int i = 0; i <= nint + 1; ++i) {
-          if (run && i < ntgt_wg) {
-            consume(i, T, r);
-            issue(i + 1, T, r);  // list i + 1: written at interval i - 1 (or the prologue)
-          }
-          lds_barrier();
-        }
-      } else {
-        LfTgt T0, T1;
-        float2 r0[CAP], r1[CAP];
-        if (run) issue(0, T0, r0);
-        for (int i = 0; i <= nint + 1; i += 2) {
-          if (run) {
-            issue(i + 1, T1, r1);  // in flight through interval i + 1's start
-            if (i < ntgt_wg) consume(i, T0, r0);
-          }
-          lds_barrier();
-          if (i + 1 <= nint + 1) {
-            if (run) {
-              issue(i + 2, T0, r0);
-              if (i + 1 < ntgt_wg) consume(i + 1, T1, r1);
-            }
-            lds_barrier();
-          }
-        }
-      }
-    }
-  } else if (PIPE && IDX && wave < GW) {
+  if (PIPE && IDX && wave < GW) {
     // ------------------------------------------------------------------ gather role, shared lists
     const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
     const int s0 = g;
@@ -5464,18 +5185,14 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   // (IDX: empty slots cost no loads, default 8: the c3 pass 17.3 -> 17.0 ms over 6)
   const char* rpe = getenv("XPG_WIDE_RP");
   const int rpf = rpe ? atoi(rpe) : idx ? 8 : 6;
-  // lane-feature gather role over the IDX lists (XPG_WIDE_LF: 1 / 2 = items issued one / two
-  // intervals ahead, 0 = the 16-lane group gather)
-  const char* lfe = getenv("XPG_WIDE_LF");
-  const int lfd = idx && lfe ? atoi(lfe) : 0;
-  // transposed MFMA product + in-lane head epilogue (XPG_WIDE_TH=1)
+  // transposed MFMA product + in-lane head epilogue (default with IDX: c3 layer 2 12.6 -> 11.9 ms
+  // per pass; XPG_WIDE_TH=0 keeps the 32-lane DPP head reduction)
   const char* the = getenv("XPG_WIDE_TH");
-  const bool th = idx && lfd == 0 && the && std::strcmp(the, "1") == 0;
+  const bool th = idx && !(the && std::strcmp(the, "0") == 0);
   if (ws2) {
-    if (pipe && idx && lfd == 1) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, 1>;
-    else if (pipe && idx && lfd == 2) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, 2>;
-    else if (pipe && idx && th && rpf == 10) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 10, true, 0, true>;
-    else if (pipe && idx && th) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, 0, true>;
+    if (pipe && idx && th && rpf == 10) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 10, true, true>;
+    else if (pipe && idx && th && rpf == 4) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 4, true, true>;
+    else if (pipe && idx && th) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 8, true, true>;
     else if (pipe && idx && rpf == 12) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 12, true>;
     else if (pipe && idx && rpf == 10) k2 = k_wide_last_ws<8, 32, 8, true, 1, true, 10, true>;
     else if (pipe && idx) k2 = rpf == 8 ? k_wide_last_ws<8, 32, 8, true, 1, true, 8, true>

@@ -79,12 +79,8 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_IDX", "0")
     else:
         monkeypatch.delenv("XPG_WIDE_IDX", raising=False)
-    if path in ("wide-lf1", "wide-lf2"):  # lane-feature gather waves, items 1 / 2 intervals ahead
-        monkeypatch.setenv("XPG_WIDE_LF", path[-1])
-    else:
-        monkeypatch.delenv("XPG_WIDE_LF", raising=False)
-    if path == "wide-th":  # transposed layer-2 product, in-lane head epilogue
-        monkeypatch.setenv("XPG_WIDE_TH", "1")
+    if path == "wide-noth":  # layer 2 without the transposed product (32-lane head reduction)
+        monkeypatch.setenv("XPG_WIDE_TH", "0")
     else:
         monkeypatch.delenv("XPG_WIDE_TH", raising=False)
 
@@ -138,8 +134,8 @@ def _masks(R, S, seed):
 
 # ------------------------------------------------------------------ hubs, all targets
 @pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "wide-teams",
-                                  "wide-nopipe", "wide-noct", "wide-rp4", "wide-noidx", "wide-lf1",
-                                  "wide-lf2", "wide-th", "unfused"])
+                                  "wide-nopipe", "wide-noct", "wide-rp4", "wide-noidx", "wide-noth",
+                                  "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1]),
@@ -253,12 +249,12 @@ def test_c3_full_graph_sampled_columns():
     iso = oracle.forward_union(spec, xn[cols], {None: (np.zeros(0, np.int64),) * 2})[:, 0]
     np.testing.assert_allclose(ysel[1, cols], iso, rtol=0, atol=1e-5)
     # every output of the first pass (32 rows x all 1M targets) of the default three-piece bf16
-    # layer 2 (and its transposed-head / lane-feature variants) against the exact-f32 MFMA
+    # layer 2 (transposed head, and the 32-lane head reduction) against the exact-f32 MFMA
     # kernel (XPG_WIDE_B3=0): the split-precision error bound over whole rows, not 48 columns
     b32 = bits[:32].contiguous()
     with _env(XPG_WIDE_B3="0"):
         y_ex = plan.forward(b32)
-    for variant in ({}, {"XPG_WIDE_TH": "1"}, {"XPG_WIDE_LF": "2"}):
+    for variant in ({}, {"XPG_WIDE_TH": "0"}):
         with _env(**variant):
             y_v = plan.forward(b32)
         d = float((y_v - y_ex).abs().max())

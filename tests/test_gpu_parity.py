@@ -30,8 +30,7 @@ def _eng():
 
 
 @pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather", "wide-exact",
-                        "wide-teams", "wide-nopipe", "wide-noct", "wide-rp4", "wide-lf1", "wide-lf2",
-                        "wide-th"])
+                        "wide-teams", "wide-nopipe", "wide-noct", "wide-rp4", "wide-noth"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
@@ -56,10 +55,8 @@ def fwd_path(request, monkeypatch):
         monkeypatch.setenv("XPG_WIDE_CT", "0")
     if request.param == "wide-rp4":
         monkeypatch.setenv("XPG_WIDE_RP", "4")
-    if request.param in ("wide-lf1", "wide-lf2"):  # lane-feature gather, items 1 / 2 intervals ahead
-        monkeypatch.setenv("XPG_WIDE_LF", request.param[-1])
-    if request.param == "wide-th":  # transposed layer-2 product, in-lane head epilogue
-        monkeypatch.setenv("XPG_WIDE_TH", "1")
+    if request.param == "wide-noth":  # layer 2 without the transposed product (32-lane head reduction)
+        monkeypatch.setenv("XPG_WIDE_TH", "0")
     return request.param
 
 
