@@ -85,6 +85,7 @@ class Explainer:
         self.last_run = None  # diagnostics of the last run (per-repeat losses, path used)
         self.group = None     # torch.distributed process group for multi-GPU runs (None = world)
         self._verified = set()  # module states whose compiled program passed verify_plan
+        self._queries = {}      # per-query (prepare context, plan, arch check): _query_key
 
     @property
     def edge_masks(self):
@@ -136,7 +137,7 @@ class Explainer:
                 "No element names have been given and the node name given is not numeric"
             return int(element)
         if isinstance(element, str):
-            members, idx = _name_index(names)
+            members, idx = _name_index(names, element)
             assert element in members, "Element name '{}' is not present in the graph".format(element)
             return idx[element]
         assert element in names, "Element name '{}' is not present in the graph".format(element)
@@ -172,6 +173,30 @@ class Explainer:
         return (id(self.arch), state, bufs, self.edge_masks, bool(getattr(plan, "multi_type", False)),
                 tuple(c["h_ntypes"] or ()), tuple(c["h_etypes"] or ()),
                 tuple(getattr(plan, "lowering", ())))
+
+    def _query_key(self, element, device):
+        """What prepare() and the query's ForwardPlan depend on: the element and problem, the
+        graph (every tensor's storage, in-place version and shape), the names / pathways /
+        type inputs (identity plus a cheap content fingerprint), the module state (parameter
+        storage and version counters) and the arch-check mode.  prepare() draws no random
+        numbers, so reusing its result leaves every RNG stream as the reference's."""
+        def ts(x):
+            if isinstance(x, dict):
+                return tuple((k, ts(v)) for k, v in x.items())
+            if isinstance(x, torch.Tensor):
+                return (x.data_ptr(), x._version, tuple(x.shape))
+            if isinstance(x, (list, tuple)):
+                n = len(x)
+                return (id(x), n) + tuple(str(x[i]) if not isinstance(x[i], (list, tuple))
+                                          else (len(x[i]),) + tuple(map(str, x[i][:1] + x[i][-1:]))
+                                          for i in (0, n // 2, n - 1) if n)
+            return id(x)
+        state = tuple((t.data_ptr(), t._version) for t in self.arch.parameters())
+        bufs = tuple((t.data_ptr(), t._version) for t in self.arch.buffers())
+        return (str(element), type(element).__name__, self.problem, self.edge_masks, str(device),
+                ts(self.feat), ts(self.edge_index), ts(self.names), ts(self.pathways),
+                ts(self.pathway_names), ts(self.node_types), ts(self.edge_types), self.element_type,
+                id(self.arch), state, bufs, str(self.params.get("verify_arch", True)))
 
     # ------------------------------------------------------------------------------ run
     def prepare(self, element, device):
@@ -259,12 +284,19 @@ class Explainer:
         sharding.sync_rng(self.group)
         self.arch = self.arch.to(device).eval()
         clock.mark("prepare")
-        c = self.prepare(element, device)
+        # a query explained again (same graph, names, module state) reuses its computational
+        # subgraph, plan and arch check: prepare() and the plan build are the run's largest host
+        # costs (explainer.py:345-480 redone by the reference on every call)
+        qkey = self._query_key(element, device) if self.params.get("plan_cache", True) else None
+        cached = self._queries.get(qkey) if qkey is not None else None
+        c = cached[0] if cached else self.prepare(element, device)
         clock.mark("plan")
         sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
 
-        if self.edge_masks:
+        if cached:
+            plan, verify = cached[1], None
+        elif self.edge_masks:
             plan = pipeline.build_edge_plan(self.arch, sub_feat, sub_ei, *c["link"])
             verify = lambda: pipeline.verify_edge_plan(plan, self.arch, sub_feat, sub_ei, *c["link"])
         else:
@@ -273,7 +305,15 @@ class Explainer:
         clock.mark("verify")
         arch_check = "off"
         mode = self.params.get("verify_arch", True)
-        if plan is not None and mode:
+        if cached:
+            arch_check = cached[2] if cached[2] in ("off", "failed") else "cached"
+            if mode == "always" and plan is not None:
+                cached = None  # checked again below
+        if plan is not None and mode and not cached:
+            if verify is None:
+                verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo) \
+                    if not self.edge_masks else pipeline.verify_edge_plan(plan, self.arch, sub_feat, sub_ei,
+                                                                          *c["link"])
             # the check guards the arch lowering (program.compile_arch + the plan's term
             # dropping), which depends on the module, the graph's type structure and the query
             # layer's node types: once per module state (parameter storage + in-place version
@@ -292,6 +332,10 @@ class Explainer:
                     arch_check = "verified"
             else:
                 arch_check = "cached"
+        if qkey is not None:
+            if len(self._queries) >= 8 and qkey not in self._queries:
+                self._queries.pop(next(iter(self._queries)))  # oldest query out
+            self._queries[qkey] = (c, plan, arch_check)
 
         clock.mark("sample")
         sampler = self.params.get("mask_sampler", "compat")
@@ -534,21 +578,31 @@ class Explainer:
 _NAME_INDEX = {}
 
 
-def _name_index(names):
+def _name_index(names, element=None):
     """(set(names), {str(name): first position}) of a names list — `element in names` and the
     reference's np.where(np.array(names, dtype=str) == element)[0][0] as lookups — cached by
-    identity and length (a list edited in place to the same length keeps a stale index)."""
+    identity and length.  A hit is validated against the list itself (the cached position of
+    `element` must still hold it, and a name missing from the cached set is looked for again),
+    so a list edited in place is re-indexed instead of answering from a stale index; an edit
+    that adds an EARLIER copy of an indexed name at the same length is not detected."""
     key = (id(names), len(names))
     hit = _NAME_INDEX.get(key)
     if hit is not None and hit[0] is names:
-        return hit[1], hit[2]
+        members, idx = hit[1], hit[2]
+        if element is None:
+            return members, idx
+        i = idx.get(element)
+        if i is not None and str(names[i]) == element:
+            return members, idx
+        if i is None and element not in names:
+            return members, idx  # truly absent: the caller's assertion reports it
     strs = np.array(names, dtype=str).tolist() if len(names) else []
     idx = {}
     for i, n in enumerate(strs):
         idx.setdefault(n, i)
     if len(_NAME_INDEX) > 8:
         _NAME_INDEX.clear()
-    _NAME_INDEX[key] = (names, set(names), idx)
+    _NAME_INDEX[key] = (names, set(strs), idx)
     return _NAME_INDEX[key][1], idx
 
 

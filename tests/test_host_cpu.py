@@ -83,6 +83,21 @@ def test_native_mt19937_matches_torch_randint(rows, cols, pre):
     assert torch.equal(after, torch.randint(0, 2 ** 31, (5,)))
 
 
+def test_extract_index_follows_in_place_name_edits():
+    """Explainer.extract_index caches a name -> position index per names list; a list edited in
+    place at the same length must not answer from the stale index."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    names = [f"n{i}" for i in range(50)]
+    assert Explainer.extract_index("n7", names) == 7
+    names[7], names[30] = "moved", "n7"          # same length, n7 now at 30
+    assert Explainer.extract_index("n7", names) == 30
+    names[3] = "fresh"
+    assert Explainer.extract_index("fresh", names) == 3
+    with pytest.raises(AssertionError):
+        Explainer.extract_index("n3", names)
+    assert Explainer.extract_index(12, None) == 12
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_prepare_matches_oracle_subgraph(name):
     exp, z, meta = build_explainer(name)
