@@ -1702,6 +1702,7 @@ struct WideArgs {
   int agg1;  // the only aggregating (non-ROOT) term, or -1 when there are several
   int64_t rstride;  // floats between consecutive source rows: w_row (tables) or 32 w_row (h1)
   int head1;  // the head is one Linear(f_out, 1) (+ act) read at column 0: fused epilogue
+  int sort_samples;  // IDX layer 2: gather groups take the target's samples active-first (see k_wide_last_ws)
   int dbg;   // diagnostics (XPG_WIDE_DBG): 1 skip dense + head, 2 skip row gathers, 4 head, 8 dense;
              // warp-specialised layer 2: 16 no MFMA, 32 no gathers, 64 no epilogue, 128 no products,
              // 512 MFMA waves without the raised issue priority
@@ -2439,7 +2440,19 @@ __device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8&
 // is LDS -> kept rows.  In-degrees past kIxEdges keep the in-place path.  Same summation order as
 // the plain gather: bitwise the same A tile.
 constexpr int kIxEdges = 32;                 // listed in-edges per target (32-bit kept masks)
-constexpr int kIxInts = 2 * kIxEdges + 8;    // src[32] | km[32] | b0 b1 tp sm mv + pad
+constexpr int kIxInts = 2 * kIxEdges + 8 + 32;  // src[32] | km[32] | b0 b1 tp sm mv + pad | order[32]
+constexpr int kIxOrder = 2 * kIxEdges + 8;       // order[g]: the sample gather group g takes
+
+// position of the n-th set bit of m (n < popc(m)): binary search on prefix popcounts
+__device__ __forceinline__ int nth_set_bit(uint32_t m, int n) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 16; w > 0; w >>= 1) {
+    const uint32_t low = pos + w >= 32 ? 0xFFFFFFFFu : ((1u << (pos + w)) - 1u);
+    if (__popc(m & low) <= n) pos += w;
+  }
+  return pos;
+}
 
 
 template <int NFI, int KW, int GW, bool B3 = false, int TEAMS = 1, bool PIPE = false, int RPF = 4,
@@ -2516,6 +2529,15 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       ix[2 * kIxEdges + 3] = qc_sm;
       ix[2 * kIxEdges + 4] = static_cast<int>(qc_mv);
     }
+    // sample order: the target's active samples (keep bit set) first, then the others, each in
+    // sample order.  A gather wave's four groups then hold samples of alike activity: a wave of
+    // masked-out samples issues no row slot at all, and a wave's slot count (the maximum over
+    // its groups' kept edges) is not raised by a busy sample among idle ones.  Per sample the
+    // edges are summed in the same order: the A tile is bitwise the same.
+    if (lane < 32) {
+      const int na = __popc(qc_mv);
+      ix[kIxOrder + lane] = lane < na ? nth_set_bit(qc_mv, lane) : nth_set_bit(~qc_mv, lane - na);
+    }
   };
   const bool ixw = IDX && wave == GW && !(a.dbg & 32);  // the index wave (MFMA wave 0)
   // TH (with IDX): the layer bias and the head's weight row in LDS after the lists ([f_out_pad]
@@ -2540,9 +2562,12 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   if (PIPE && IDX && wave < GW) {
     // ------------------------------------------------------------------ gather role, shared lists
     const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
-    const int s0 = g;
-    const bool v0 = s0 < a.nr;
+    // the group's sample of the current target (p_s0: the list's order with sort_samples, else
+    // sample g) and of the prefetched one
+    int s0 = g;
+    bool v0 = s0 < a.nr;
     const float* base0 = a.src + (int64_t)(v0 ? s0 : 0) * a.w_row;
+    int p_s0 = g;
     constexpr int64_t RS = 32 * 16 * NFI;  // h1 row stride (node-major: 32 samples x w_row floats)
     const int kroot = 1 - kagg;            // host-checked: terms {MEAN, ROOT}
     constexpr int RP = RPF;
@@ -2564,14 +2589,18 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       const int* ix = IX + (k % 3) * kIxInts;
       const int b0 = ix[2 * kIxEdges], b1 = ix[2 * kIxEdges + 1], tp = ix[2 * kIxEdges + 2];
       const uint32_t mv = static_cast<uint32_t>(ix[2 * kIxEdges + 4]);
-      const bool tk = v0 && ((mv >> s0) & 1u);
+      const int sk = a.sort_samples ? ix[kIxOrder + g] : g;  // group-uniform
+      const bool vk = sk < a.nr;
+      const float* bk = a.src + (int64_t)(vk ? sk : 0) * a.w_row;
+      p_s0 = sk;
+      const bool tk = vk && ((mv >> sk) & 1u);
       const int ne = min(b1 - b0, kIxEdges);
       uint32_t M = 0u;
 #pragma unroll
       for (int c = 0; c < kIxEdges / 16; ++c) {
         if (16 * c < ne) {  // workgroup-uniform
           const uint32_t km = 16 * c + gl < ne ? static_cast<uint32_t>(ix[kIxEdges + 16 * c + gl]) : 0u;
-          M |= (static_cast<uint32_t>(__ballot(tk && ((km >> s0) & 1u)) >> lb) & 0xFFFFu) << (16 * c);
+          M |= (static_cast<uint32_t>(__ballot(tk && ((km >> sk) & 1u)) >> lb) & 0xFFFFu) << (16 * c);
         }
       }
       p_cnt = __popc(M);
@@ -2579,8 +2608,8 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       p_sm = ix[2 * kIxEdges + 3];
       p_b0 = b0;
       p_b1 = b1;
-      const float* p0r = a.ctab && !((mv >> s0) & 1u) ? a.ctab + (int64_t)tp * a.w_row + fo
-                                                       : base0 + (int64_t)tp * RS + fo;
+      const float* p0r = a.ctab && !((mv >> sk) & 1u) ? a.ctab + (int64_t)tp * a.w_row + fo
+                                                       : bk + (int64_t)tp * RS + fo;
       int fill = 0;
 #pragma unroll
       for (int jj = 0; jj < RP; ++jj) {
@@ -2589,7 +2618,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
           fill = jj + 1;
           if (M) {
             const int j = __builtin_ctz(M);
-            const float* sp = base0 + (int64_t)ix[j] * RS + fo;
+            const float* sp = bk + (int64_t)ix[j] * RS + fo;
 #pragma unroll
             for (int x = 0; x < NFI / 4; ++x) {
               const float4 v = reinterpret_cast<const float4*>(sp)[x];
@@ -2617,6 +2646,9 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     if (run) prefetch(0);
     for (int i = 0; i <= nint + 1; ++i) {
       if (run && i < ntgt_wg) {
+        s0 = p_s0;  // the sample of target i (set by its prefetch)
+        v0 = s0 < a.nr;
+        base0 = a.src + (int64_t)(v0 ? s0 : 0) * a.w_row;
         float acc[NFI];
 #pragma unroll
         for (int x = 0; x < NFI; ++x) acc[x] = 0.f;
@@ -5187,6 +5219,9 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const int rpf = rpe ? atoi(rpe) : idx ? 8 : 6;
   // transposed MFMA product + in-lane head epilogue (default with IDX: c3 layer 2 12.6 -> 11.9 ms
   // per pass; XPG_WIDE_TH=0 keeps the 32-lane DPP head reduction)
+  // gather groups take each target's samples active-first (XPG_WIDE_SORT=0: sample g)
+  const char* soe = getenv("XPG_WIDE_SORT");
+  a2.sort_samples = idx && !(soe && std::strcmp(soe, "0") == 0) ? 1 : 0;
   const char* the = getenv("XPG_WIDE_TH");
   const bool th = idx && !(the && std::strcmp(the, "0") == 0);
   if (ws2) {

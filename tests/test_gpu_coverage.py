@@ -83,6 +83,10 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_TH", "0")
     else:
         monkeypatch.delenv("XPG_WIDE_TH", raising=False)
+    if path == "wide-nosort":  # gather group g takes sample g (no active-first order)
+        monkeypatch.setenv("XPG_WIDE_SORT", "0")
+    else:
+        monkeypatch.delenv("XPG_WIDE_SORT", raising=False)
 
 
 @contextlib.contextmanager
@@ -135,7 +139,7 @@ def _masks(R, S, seed):
 # ------------------------------------------------------------------ hubs, all targets
 @pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "wide-teams",
                                   "wide-nopipe", "wide-noct", "wide-rp4", "wide-noidx", "wide-noth",
-                                  "unfused"])
+                                  "wide-nosort", "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1]),
