@@ -1703,6 +1703,7 @@ struct WideArgs {
   int64_t rstride;  // floats between consecutive source rows: w_row (tables) or 32 w_row (h1)
   int head1;  // the head is one Linear(f_out, 1) (+ act) read at column 0: fused epilogue
   int sort_samples;  // IDX layer 2: gather groups take the target's samples active-first (see k_wide_last_ws)
+  int early_prefetch;  // IDX layer 2: the next target's rows are issued before the A tile is finished
   int dbg;   // diagnostics (XPG_WIDE_DBG): 1 skip dense + head, 2 skip row gathers, 4 head, 8 dense;
              // warp-specialised layer 2: 16 no MFMA, 32 no gathers, 64 no epilogue, 128 no products,
              // 512 MFMA waves without the raised issue priority
@@ -2432,13 +2433,50 @@ __device__ __forceinline__ void split_bf16x8(const float* x, bf16x8& hi, bf16x8&
 // Same summation order as the plain gather (bitwise the same A tile).
 // IDX (with PIPE): the target's index work is done ONCE per workgroup instead of by each of the 32
 // gather groups (they all read the same CSR range, edge list and keep words, which hold every
-// sample's bit): MFMA wave 0 -- idle most of each interval -- runs that chain two targets ahead
-// (CSR range -> first kIxEdges in-edges -> keep words, software-pipelined one stage per
-// interval) and leaves per target the edges' source rows and 32-sample kept masks
+// sample's bit): MFMA wave 0 -- idle most of each interval -- runs that chain ahead of the
+// gathers (CSR range -> first kIxEdges in-edges -> keep words, software-pipelined one stage per
+// interval, each stage's loads consumed an interval after their issue) and leaves per target the edges' source rows and 32-sample kept masks
 // (source keep word & target keep word) in an LDS ring of three lists.  A gather group then
 // reads its kept edges from the list (ballots over the mask bits), so its own chain per target
 // is LDS -> kept rows.  In-degrees past kIxEdges keep the in-place path.  Same summation order as
 // the plain gather: bitwise the same A tile.
+// XPG_WIDE_DIAG (a diagnostics build only, never the product library): XPG_WIDE_DBG 1024 reads
+// every gathered h1 row from the first 64 nodes (L2-resident: the gather's cost without HBM),
+// 2048 drops the kept edges past the prefetched ones (the in-place rounds' cost).
+// XPG_WIDE_STAMPS (a diagnostics build only): per-wave cycle counts of the layer-2 phases
+// (s_memtime), per workgroup, read back with xpg_debug_wide_stamps (tools/ws_stamps.py)
+#ifdef XPG_WIDE_STAMPS
+__device__ uint64_t g_wide_stamps[512][16][8];
+#define XPG_WST_INIT                                                       \
+  uint64_t wst_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};                          \
+  uint64_t wst_last = __builtin_amdgcn_s_memtime();
+#define XPG_WST(k)                                                         \
+  {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();                    \
+    wst_acc[k] += now_ - wst_last;                                         \
+    wst_last = now_;                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+  }
+// lane-indexed (vector) stores of the wave's totals
+#define XPG_WST_STORE                                                      \
+  if (blockIdx.x < 512 && lane < 8) {                                      \
+    uint64_t v_ = 0;                                                       \
+    for (int q_ = 0; q_ < 8; ++q_) v_ = lane == q_ ? wst_acc[q_] : v_;     \
+    g_wide_stamps[blockIdx.x][wave][lane] = v_;                            \
+  }
+#else
+#define XPG_WST_INIT
+#define XPG_WST(k)
+#define XPG_WST_STORE
+#endif
+#ifdef XPG_WIDE_DIAG
+#define XPG_WDIAG_ROW(r) ((a.dbg & 1024) ? ((r) & 63) : (r))
+#define XPG_WDIAG_REST(m) ((a.dbg & 2048) ? 0u : (m))
+#else
+#define XPG_WDIAG_ROW(r) (r)
+#define XPG_WDIAG_REST(m) (m)
+#endif
 constexpr int kIxEdges = 32;                 // listed in-edges per target (32-bit kept masks)
 constexpr int kIxInts = 2 * kIxEdges + 8 + 32;  // src[32] | km[32] | b0 b1 tp sm mv + pad | order[32]
 constexpr int kIxOrder = 2 * kIxEdges + 8;       // order[g]: the sample gather group g takes
@@ -2488,52 +2526,59 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
   static_assert(!IDX || PIPE, "shared index lists: pipelined gather only");
   const int32_t* smul_all = a.self_mult + (int64_t)ragg * a.n_tgt;
   // ---- IDX index chain (MFMA wave 0, lane = listed edge): stage A = CSR range / target fields,
-  // B = the first kIxEdges edges' sources, C = keep words -> the LDS list of the target
-  int qa_b0 = 0, qa_b1 = 0, qa_tf0 = 0, qa_tp = 0, qa_sm = 0;
-  int qb_b0 = 0, qb_b1 = 0, qb_tf0 = 0, qb_tp = 0, qb_sm = 0, qb_src = 0, qb_u0 = 0;
-  int qc_b0 = 0, qc_b1 = 0, qc_tp = 0, qc_sm = 0, qc_src = 0;
-  uint32_t qc_mv = 0u, qc_em = 0u;
+  // B = the first kIxEdges edges' sources, C = keep words -> the LDS list of the target.  Every
+  // load is a vector load, also the target's own fields (lanes 0-4: CSR begin / end, first-layer
+  // position, previous-layer position, self count; lane 32 of stage C: the target's keep word):
+  // a wave-uniform address compiles to a scalar load, and lgkmcnt counts scalar loads together
+  // with LDS accesses, so each LDS wait of the wave (the list stores, the logit reads, the MFMA
+  // operand reads) waited for the chain's loads from HBM too
+  int qa_v = 0, qb_v = 0, qb_src = 0, qb_u0 = 0, qc_v = 0, qc_src = 0;
+  uint32_t qc_em = 0u;
   auto stA = [&](int k) {
     if (k >= ntgt_wg) return;
     const int t = blockIdx.x + k * gridDim.x;
-    qa_b0 = aptr[t];
-    qa_b1 = aptr[t + 1];
-    qa_tf0 = a.tgt_f0[t];
-    qa_tp = a.tgt_prev[t];
-    qa_sm = smul_all[t];
+    const int32_t* pa = lane < 2 ? aptr + t + lane : lane == 2 ? a.tgt_f0 + t : lane == 3 ? a.tgt_prev + t
+                                                                                            : smul_all + t;
+    qa_v = *pa;
   };
   auto stB = [&](int k) {
     if (k >= ntgt_wg) return;
-    qb_b0 = qa_b0; qb_b1 = qa_b1; qb_tf0 = qa_tf0; qb_tp = qa_tp; qb_sm = qa_sm;
-    const int e = qa_b0 + lane;
-    qb_src = e < qa_b1 && lane < kIxEdges ? a.agg_src[e] : 0;
-    qb_u0 = e < qa_b1 && lane < kIxEdges ? a.agg_f0[e] : 0;
+    qb_v = qa_v;
+    const int b0 = __builtin_amdgcn_readlane(qa_v, 0), b1 = __builtin_amdgcn_readlane(qa_v, 1);
+    const int tf0 = __builtin_amdgcn_readlane(qa_v, 2);
+    const int e = b0 + lane;
+    qb_src = e < b1 && lane < kIxEdges ? a.agg_src[e] : 0;
+    qb_u0 = lane < kIxEdges ? (e < b1 ? a.agg_f0[e] : 0) : tf0;  // lanes >= kIxEdges: the target
   };
   auto stC_load = [&](int k) {
     if (k >= ntgt_wg) return;
-    qc_b0 = qb_b0; qc_b1 = qb_b1; qc_tp = qb_tp; qc_sm = qb_sm; qc_src = qb_src;
-    qc_mv = a.mT0[qb_tf0];
-    qc_em = qb_b0 + lane < qb_b1 && lane < kIxEdges ? a.mT0[qb_u0] : 0u;
+    qc_v = qb_v;
+    qc_src = qb_src;
+    qc_em = a.mT0[qb_u0];
   };
   auto stC_store = [&](int k) {
     if (k >= ntgt_wg) return;
     int* ix = IX + (k % 3) * kIxInts;
+    const int b0 = __builtin_amdgcn_readlane(qc_v, 0), b1 = __builtin_amdgcn_readlane(qc_v, 1);
+    const uint32_t qc_mv = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(qc_em), kIxEdges));
     if (lane < kIxEdges) {
       ix[lane] = qc_src;
-      ix[kIxEdges + lane] = static_cast<int>(qc_em & qc_mv);
+      ix[kIxEdges + lane] = b0 + lane < b1 ? static_cast<int>(qc_em & qc_mv) : 0;
     }
     if (lane == 0) {
-      ix[2 * kIxEdges] = qc_b0;
-      ix[2 * kIxEdges + 1] = qc_b1;
-      ix[2 * kIxEdges + 2] = qc_tp;
-      ix[2 * kIxEdges + 3] = qc_sm;
+      ix[2 * kIxEdges] = b0;
+      ix[2 * kIxEdges + 1] = b1;
+      ix[2 * kIxEdges + 2] = __builtin_amdgcn_readlane(qc_v, 3);
+      ix[2 * kIxEdges + 3] = __builtin_amdgcn_readlane(qc_v, 4);
       ix[2 * kIxEdges + 4] = static_cast<int>(qc_mv);
     }
     // sample order: the target's active samples (keep bit set) first, then the others, each in
     // sample order.  A gather wave's four groups then hold samples of alike activity: a wave of
     // masked-out samples issues no row slot at all, and a wave's slot count (the maximum over
     // its groups' kept edges) is not raised by a busy sample among idle ones.  Per sample the
-    // edges are summed in the same order: the A tile is bitwise the same.
+    // edges are summed in the same order: the A tile is bitwise the same.  (Ordering by kept
+    // count instead packs the slot loads fuller, 0.8 of their lanes against 0.6, but the index
+    // wave's per-sample counts and sort cost more than the loads saved: profiles/r4_cntsort.log)
     if (lane < 32) {
       const int na = __popc(qc_mv);
       ix[kIxOrder + lane] = lane < na ? nth_set_bit(qc_mv, lane) : nth_set_bit(~qc_mv, lane - na);
@@ -2551,11 +2596,13 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     }
   }
   if constexpr (IDX) {
-    // prologue: the lists of targets 0 and 1, the chain state of targets 2 (B) and 3 (A)
+    // prologue: the lists of targets 0 and 1, the chain state of targets 2 (C: stored at the
+    // start of interval 0), 3 (B) and 4 (A)
     if (ixw) {
       stA(0); stB(0); stC_load(0); stC_store(0);
       stA(1); stB(1); stC_load(1); stC_store(1);
-      stA(2); stB(2); stA(3);
+      stA(2); stB(2); stC_load(2);
+      stA(3); stB(3); stA(4);
     }
     lds_barrier();
   }
@@ -2576,20 +2623,35 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     uint32_t p_rest = 0u;
     int p_cnt = 0, p_sm = 0, p_b0 = 0, p_b1 = 0, p_fill = 0;
     bool p_tk = false;
-    float p_cv[RP], p_row[RP][NFI], p_self[NFI];
+    // the own rows of the current and the prefetched target alternate between two arrays (the
+    // loop runs two targets per trip): a loaded array that is not the one the next trip reads
+    // would be copied at the back edge, after a wait for every load in flight
+    float p_cv[RP], p_row[RP][NFI], p_selfA[NFI], p_selfB[NFI];
 #pragma unroll
     for (int jj = 0; jj < RP; ++jj)
 #pragma unroll
       for (int x = 0; x < NFI; ++x) p_row[jj][x] = 0.f;  // slots keep finite values: 0 x stale row = 0
+    XPG_WST_INIT
     // the next target's kept edges from its list (wave-uniform k: the ballots see every lane),
     // its first RP kept rows (slot jj loaded only by the groups with a jj-th kept edge, and only
     // while some group of the wave has one) and its own row in flight
-    auto prefetch = [&](int k) {
+    auto prefetch = [&](int k, float (&p_self)[NFI]) {
       if (k >= ntgt_wg) return;
       const int* ix = IX + (k % 3) * kIxInts;
+      // every LDS read of the list is issued up front and waited for once: read one after another
+      // behind the branches that use them, each paid the LDS latency in turn (the list header,
+      // the sample order, each 16-edge chunk of kept masks, then each slot's source row)
       const int b0 = ix[2 * kIxEdges], b1 = ix[2 * kIxEdges + 1], tp = ix[2 * kIxEdges + 2];
+      const int smk = ix[2 * kIxEdges + 3];
       const uint32_t mv = static_cast<uint32_t>(ix[2 * kIxEdges + 4]);
-      const int sk = a.sort_samples ? ix[kIxOrder + g] : g;  // group-uniform
+      const int ord = ix[kIxOrder + g];
+      uint32_t kmc[kIxEdges / 16];
+#pragma unroll
+      for (int c = 0; c < kIxEdges / 16; ++c) kmc[c] = static_cast<uint32_t>(ix[kIxEdges + 16 * c + gl]);
+#pragma unroll
+      for (int c = 0; c < kIxEdges / 16; ++c) asm volatile("" ::"v"(kmc[c]));  // not sunk into the branches
+      XPG_WST(6)
+      const int sk = a.sort_samples ? ord : g;  // group-uniform
       const bool vk = sk < a.nr;
       const float* bk = a.src + (int64_t)(vk ? sk : 0) * a.w_row;
       p_s0 = sk;
@@ -2599,17 +2661,30 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
 #pragma unroll
       for (int c = 0; c < kIxEdges / 16; ++c) {
         if (16 * c < ne) {  // workgroup-uniform
-          const uint32_t km = 16 * c + gl < ne ? static_cast<uint32_t>(ix[kIxEdges + 16 * c + gl]) : 0u;
+          const uint32_t km = 16 * c + gl < ne ? kmc[c] : 0u;
           M |= (static_cast<uint32_t>(__ballot(tk && ((km >> sk) & 1u)) >> lb) & 0xFFFFu) << (16 * c);
         }
       }
       p_cnt = __popc(M);
       p_tk = tk;
-      p_sm = ix[2 * kIxEdges + 3];
+      p_sm = smk;
       p_b0 = b0;
       p_b1 = b1;
       const float* p0r = a.ctab && !((mv >> sk) & 1u) ? a.ctab + (int64_t)tp * a.w_row + fo
-                                                       : bk + (int64_t)tp * RS + fo;
+                                                       : bk + (int64_t)XPG_WDIAG_ROW(tp) * RS + fo;
+      // the source rows of the group's first RP kept edges (slot jj: the jj-th set bit of M)
+      int srcs[RP];
+      {
+        uint32_t Mx = M;
+#pragma unroll
+        for (int jj = 0; jj < RP; ++jj) {
+          srcs[jj] = ix[Mx ? __builtin_ctz(Mx) : 0];
+          Mx &= Mx - 1u;
+        }
+#pragma unroll
+        for (int jj = 0; jj < RP; ++jj) asm volatile("" ::"v"(srcs[jj]));  // all reads issued here
+      }
+      XPG_WST(7)
       int fill = 0;
 #pragma unroll
       for (int jj = 0; jj < RP; ++jj) {
@@ -2617,8 +2692,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         if (__ballot(M != 0u) != 0ull) {  // wave-uniform: some group has a jj-th kept edge
           fill = jj + 1;
           if (M) {
-            const int j = __builtin_ctz(M);
-            const float* sp = bk + (int64_t)ix[j] * RS + fo;
+            const float* sp = bk + (int64_t)XPG_WDIAG_ROW(srcs[jj]) * RS + fo;
 #pragma unroll
             for (int x = 0; x < NFI / 4; ++x) {
               const float4 v = reinterpret_cast<const float4*>(sp)[x];
@@ -2643,8 +2717,8 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       }
     };
     const bool run = !(a.dbg & 32);  // dbg 32 (diagnostics): no gathers
-    if (run) prefetch(0);
-    for (int i = 0; i <= nint + 1; ++i) {
+    if (run) prefetch(0, p_selfA);
+    auto step = [&](int i, float (&p_self)[NFI], float (&p_next)[NFI]) {
       if (run && i < ntgt_wg) {
         s0 = p_s0;  // the sample of target i (set by its prefetch)
         v0 = s0 < a.nr;
@@ -2658,9 +2732,10 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
 #pragma unroll
             for (int x = 0; x < NFI; ++x) acc[x] = fmaf(p_cv[q], p_row[q][x], acc[x]);
           }
+        XPG_WST(1)
         // listed kept edges past the prefetched ones, in place (ctz order), RI rows per round
         const int* ix = IX + (i % 3) * kIxInts;
-        uint32_t m = p_rest;
+        uint32_t m = XPG_WDIAG_REST(p_rest);
         while (m) {  // group-uniform
           float rr[RI][NFI];
           float cv[RI];
@@ -2669,7 +2744,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
             const int j = m ? __builtin_ctz(m) : 0;
             cv[q] = m ? 1.f : 0.f;
             m &= m - 1u;
-            const float* sp = base0 + (int64_t)ix[j] * RS + fo;
+            const float* sp = base0 + (int64_t)XPG_WDIAG_ROW(ix[j]) * RS + fo;
 #pragma unroll
             for (int x = 0; x < NFI / 4; ++x) {
               const float4 v = reinterpret_cast<const float4*>(sp)[x];
@@ -2702,7 +2777,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
               cv[q] = mm ? 1.f : 0.f;
               mm &= mm - 1u;
               const int srow = __shfl(esrc, lb + j, 64);
-              const float* sp = base0 + (int64_t)srow * RS + fo;
+              const float* sp = base0 + (int64_t)XPG_WDIAG_ROW(srow) * RS + fo;
 #pragma unroll
               for (int x = 0; x < NFI / 4; ++x) {
                 const float4 v = reinterpret_cast<const float4*>(sp)[x];
@@ -2718,32 +2793,54 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
               for (int x = 0; x < NFI; ++x) acc[x] = fmaf(cv[q], rr[q][x], acc[x]);
           }
         }
-        const float inv = p_tk ? 1.f / static_cast<float>(max(cnt + p_sm, 1)) : 0.f;
-        float self[NFI];
-#pragma unroll
-        for (int x = 0; x < NFI; ++x) {
-          self[x] = p_self[x];
-          acc[x] = fmaf(static_cast<float>(p_sm), self[x], acc[x]) * inv;
-        }
+        // every load of target i has been consumed: the own row goes into the ROOT columns of the
+        // A tile and into the mean's sum first, so no register of target i is live across the
+        // next target's loads (a loaded register still live there costs a copy at the loop's back
+        // edge, i.e. a wait for every load in flight before the barrier); with early_prefetch the
+        // next target's rows then go out and the mean, the bf16 split and the A stores of the
+        // aggregate run while they are in flight
         __bf16* A = Ab + (i & 1) * 2 * abuf;  // abuf floats = 2 abuf bf16
-        bf16x8 hi, lo;
+        const int sm_i = p_sm;
+        const bool tk_i = p_tk;
+        XPG_WST(2)
+        {
+          float self[NFI];
 #pragma unroll
-        for (int x = 0; x < NFI; ++x) {
-          acc[x] = v0 ? acc[x] : 0.f;
-          self[x] = v0 ? self[x] : 0.f;
+          for (int x = 0; x < NFI; ++x) {
+            acc[x] = fmaf(static_cast<float>(sm_i), p_self[x], acc[x]);
+            self[x] = v0 ? p_self[x] : 0.f;
+          }
+          bf16x8 hi, lo;
+          split_bf16x8(self, hi, lo);
+          const int er = s0 * aph + kroot * a.w_row + fo;
+          *reinterpret_cast<bf16x8*>(A + er) = hi;
+          *reinterpret_cast<bf16x8*>(A + 32 * aph + er) = lo;
         }
-        split_bf16x8(acc, hi, lo);
-        const int ea = s0 * aph + kagg * a.w_row + fo;
-        *reinterpret_cast<bf16x8*>(A + ea) = hi;
-        *reinterpret_cast<bf16x8*>(A + 32 * aph + ea) = lo;
-        split_bf16x8(self, hi, lo);
-        const int er = s0 * aph + kroot * a.w_row + fo;
-        *reinterpret_cast<bf16x8*>(A + er) = hi;
-        *reinterpret_cast<bf16x8*>(A + 32 * aph + er) = lo;
-        prefetch(i + 1);  // list of target i + 1: written at interval i - 1 (or the prologue)
+        XPG_WST(3)
+        if (a.early_prefetch) prefetch(i + 1, p_next);  // list of target i + 1: written at interval i - 1
+        XPG_WST(4)
+        const float inv = tk_i ? 1.f / static_cast<float>(max(cnt + sm_i, 1)) : 0.f;
+        {
+          bf16x8 hi, lo;
+#pragma unroll
+          for (int x = 0; x < NFI; ++x) acc[x] = v0 ? acc[x] * inv : 0.f;
+          split_bf16x8(acc, hi, lo);
+          const int ea = s0 * aph + kagg * a.w_row + fo;
+          *reinterpret_cast<bf16x8*>(A + ea) = hi;
+          *reinterpret_cast<bf16x8*>(A + 32 * aph + ea) = lo;
+        }
+        XPG_WST(5)
+        if (!a.early_prefetch) prefetch(i + 1, p_next);  // list of target i + 1: written at interval i - 1 (or the prologue)
+        XPG_WST(4)
       }
       lds_barrier();
+      XPG_WST(0)
+    };
+    for (int i = 0; i <= nint + 1; i += 2) {
+      step(i, p_selfA, p_selfB);
+      if (i + 1 <= nint + 1) step(i + 1, p_selfB, p_selfA);
     }
+    XPG_WST_STORE
   } else if (PIPE && wave < GW) {
     // ------------------------------------------------------------------ pipelined gather role
     const int g = tid >> 4, gl = tid & 15, fo = gl * NFI, lb = lane & 48;
@@ -3097,6 +3194,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     const float bv = active && col < a.f_out ? a.bias[col] : 0.f;
     const float hwc = active && col < a.f_out ? a.H[0].weight[col] : 0.f;
     const float hb = a.H[0].bias[0];
+    const int hact = a.H[0].act;
     const float* wp = a.weight + (int64_t)(active ? col : 0) * a.K + 4 * h;
     const int klast = a.K - 8;
     auto ldw = [&](int k) { return *reinterpret_cast<const float4*>(wp + (k < klast ? k : klast)); };
@@ -3125,24 +3223,54 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         }
       }
     }
+    XPG_WST_INIT
     for (int i = 0; i <= nint + 1; ++i) {
-      if (ixw) {  // index chain: keep words of i + 2 (stored below), edges of i + 3, range of i + 4
-        stC_load(i + 2);
-        stB(i + 3);
-        stA(i + 4);
+      if (ixw) {
+        // index chain, every stage's loads consumed one interval after they were issued: the
+        // list of target i + 2 (its keep words loaded during interval i - 1; the slot held the
+        // list of target i - 1, done with at the last barrier), then the keep words of i + 3,
+        // the edges of i + 4 and the CSR range of i + 5
+        stC_store(i + 2);
+        // every value the new loads need (loaded during the last interval) is read before any of
+        // them is issued: vmcnt counts in issue order, so a wait placed after a new load would
+        // wait for that load's whole HBM latency too
+        const int va = qa_v, vb = qb_v, srcb = qb_src, u0b = qb_u0;
+        const int a_b0 = __builtin_amdgcn_readlane(va, 0), a_b1 = __builtin_amdgcn_readlane(va, 1);
+        const int a_tf0 = __builtin_amdgcn_readlane(va, 2);
+        asm volatile("" ::"v"(vb), "v"(srcb), "v"(u0b), "s"(a_b0), "s"(a_b1), "s"(a_tf0));
+        if (i + 3 < ntgt_wg) {  // stage C of target i + 3: keep words
+          qc_v = vb;
+          qc_src = srcb;
+          qc_em = a.mT0[u0b];
+        }
+        if (i + 4 < ntgt_wg) {  // stage B of target i + 4: in-edges
+          qb_v = va;
+          const int e = a_b0 + lane;
+          qb_src = e < a_b1 && lane < kIxEdges ? a.agg_src[e] : 0;
+          qb_u0 = lane < kIxEdges ? (e < a_b1 ? a.agg_f0[e] : 0) : a_tf0;
+        }
+        stA(i + 5);
       }
+      XPG_WST(1)
 #pragma unroll
       for (int j = 0; j < TEAMS; ++j) {  // targets of interval i - 2: y[s] = act(sum over blocks + b)
         const int idx = TEAMS * (i - 2) + j;
         if (nb == 0 && i >= 2 && idx < ntgt_wg && lane < a.nr) {
           // written at interval i - 1 into buffer (i - 2) & 1 = i & 1
           const float* hp = H0 + ((i & 1) * TEAMS + j) * a.f_out_pad;
+          // the column blocks' partials read at once (f_out_pad <= 128: four MFMA waves of 32
+          // columns), summed in block order
+          float hv[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) hv[b] = hp[min(b * 32, a.f_out_pad - 32) + lane];
           float v = 0.f;
-          for (int b = 0; b * 32 < a.f_out_pad; ++b) v += hp[b * 32 + lane];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) v = b * 32 < a.f_out_pad ? v + hv[b] : v;
           const int tf = blockIdx.x + idx * gridDim.x;
-          a.out[(a.row0 + lane) * a.n_tgt + tf] = act_apply(v + hb, a.H[0].act);
+          a.out[(a.row0 + lane) * a.n_tgt + tf] = act_apply(v + hb, hact);
         }
       }
+      XPG_WST(2)
       for (int j = 0; j < TEAMS; ++j) {
       const int slot = ((i - 1) & 1) * TEAMS + j;
       if (i >= 1 && TEAMS * (i - 1) + j < ntgt_wg && active && !(a.dbg & 16)) {  // dbg 16 (diagnostics): no MFMA
@@ -3236,6 +3364,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         }
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
+        XPG_WST(3)
         if constexpr (TH) {
           // column c = nb * 32 + (reg & 3) + 8 (reg >> 2) + 4 h of sample i32 sits in acc[reg]:
           // the head dot over the wave's 32 columns is 16 in-lane FMAs plus one swap of the two
@@ -3293,9 +3422,11 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         }  // !TH
       }
       }
-      if (ixw) stC_store(i + 2);  // the list of target i + 2 (read from interval i + 1 on)
+      XPG_WST(4)
       lds_barrier();
+      XPG_WST(0)
     }
+    XPG_WST_STORE
   }
 }
 
@@ -5129,7 +5260,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
     }
     if (nagg != 1) a.agg1 = -1;
   };
-  WideArgs a1, a2;
+  WideArgs a1{}, a2{};
   fill(a1, l1);
   if (const int rc = diag_env("XPG_WIDE_DBG", &a1.dbg)) return rc;
   a1.n_src = p->n0;
@@ -5222,6 +5353,9 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   // gather groups take each target's samples active-first (XPG_WIDE_SORT=0: sample g)
   const char* soe = getenv("XPG_WIDE_SORT");
   a2.sort_samples = idx && !(soe && std::strcmp(soe, "0") == 0) ? 1 : 0;
+  // the next target's rows issued before the A tile's finishing arithmetic (XPG_WIDE_EARLY=0: after)
+  const char* eae = getenv("XPG_WIDE_EARLY");
+  a2.early_prefetch = idx && !(eae && std::strcmp(eae, "0") == 0) ? 1 : 0;
   const char* the = getenv("XPG_WIDE_TH");
   const bool th = idx && !(the && std::strcmp(the, "0") == 0);
   if (ws2) {
@@ -5490,6 +5624,13 @@ int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t
   if (rows > 0) hostrng::mask_bits(state, left, next, rows, cols, bits);
   return XPG_OK;
 }
+
+#ifdef XPG_WIDE_STAMPS  // diagnostic build only: layer-2 phase cycles [512 workgroups][16 waves][8]
+int xpg_debug_wide_stamps(uint64_t* out) {
+  XPG_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wide_stamps), sizeof(uint64_t) * 512 * 16 * 8));
+  return XPG_OK;
+}
+#endif
 
 #ifdef XPG_WLM_STAMPS  // diagnostic build only: per-phase cycle stamps of the last stamped launch
 int xpg_debug_stamps(uint64_t* out) {

@@ -87,6 +87,10 @@ def _force(monkeypatch, path):
         monkeypatch.setenv("XPG_WIDE_SORT", "0")
     else:
         monkeypatch.delenv("XPG_WIDE_SORT", raising=False)
+    if path == "wide-late":  # the next target's rows issued after the A tile is stored
+        monkeypatch.setenv("XPG_WIDE_EARLY", "0")
+    else:
+        monkeypatch.delenv("XPG_WIDE_EARLY", raising=False)
 
 
 @contextlib.contextmanager
@@ -139,7 +143,7 @@ def _masks(R, S, seed):
 # ------------------------------------------------------------------ hubs, all targets
 @pytest.mark.parametrize("path", ["wide", "wide-mfma", "wide-gather", "wide-exact", "wide-teams",
                                   "wide-nopipe", "wide-noct", "wide-rp4", "wide-noidx", "wide-noth",
-                                  "wide-nosort", "unfused"])
+                                  "wide-nosort", "wide-late", "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("sage", [16, 64, 64], [64, 1]),
                                            ("gcn", [16, 32, 64], [64, 8, 1]),
                                            ("sage", [24, 128, 128], [128, 16, 1]),

@@ -31,7 +31,7 @@ def _eng():
 
 @pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather", "wide-exact",
                         "wide-teams", "wide-nopipe", "wide-noct", "wide-rp4", "wide-noth",
-                        "wide-nosort"])
+                        "wide-nosort", "wide-late"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
@@ -60,6 +60,8 @@ def fwd_path(request, monkeypatch):
         monkeypatch.setenv("XPG_WIDE_TH", "0")
     if request.param == "wide-nosort":  # gather group g takes sample g (no active-first order)
         monkeypatch.setenv("XPG_WIDE_SORT", "0")
+    if request.param == "wide-late":  # the next target's rows issued after the A tile is stored
+        monkeypatch.setenv("XPG_WIDE_EARLY", "0")
     return request.param
 
 

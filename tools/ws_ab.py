@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bikg_graph_explainability_public_amd import _lib, engine, pipeline  # noqa: E402
 from bikg_graph_explainability_public_amd.nn import ConvStack  # noqa: E402
 
-KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW", "DBG", "PIPE", "RP", "CT", "IDX", "TH", "SORT")
+KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW", "DBG", "PIPE", "RP", "CT", "IDX", "TH", "SORT", "EARLY")
 
 
 def set_env(spec):
