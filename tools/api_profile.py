@@ -35,11 +35,19 @@ def main():
     exp = Explainer(feat.to(dev), ei.to(dev), arch, params, [str(i) for i in range(n)])
     exp.run("8", args.times)
     torch.cuda.synchronize()
-    for q in ("9", "10"):
-        t0 = time.perf_counter()
-        exp.run(q, args.times)
-        torch.cuda.synchronize()
-        print(f"run({q}, {args.times}): {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
+    for cache in (True, False):
+        exp.params["plan_cache"] = cache
+        for q in ("9", "10", "10", "11"):
+            a0 = torch.cuda.memory_stats().get("num_device_alloc", -1)
+            t0 = time.perf_counter()
+            exp.run(q, args.times)
+            torch.cuda.synchronize()
+            a1 = torch.cuda.memory_stats().get("num_device_alloc", -1)
+            ph = exp.last_run["phases"].times()
+            print(f"plan_cache={cache} run({q}, {args.times}): {(time.perf_counter() - t0) * 1e3:.2f} ms, "
+                  f"device allocations {a1 - a0}, phases "
+                  f"{ {k: round(v['host_ms'], 2) for k, v in ph.items() if isinstance(v, dict)} }", flush=True)
+    exp.params["plan_cache"] = True
     pr = cProfile.Profile()
     pr.enable()
     exp.run("7", args.times)
