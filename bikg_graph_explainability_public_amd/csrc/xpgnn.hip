@@ -3586,6 +3586,9 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
         }
       }
     }
+    // MEAN: lane s computes sample s's 1 / (kept count + self count) once for all samples (the
+    // division per sample on wave-uniform operands cost ~10 VALU instructions x 32 per target)
+    const float inv_l = !GCN && ((mv >> (lane & 31)) & 1u) ? 1.f / static_cast<float>(max(cnt_l + sm, 1)) : 0.f;
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
       if (GCN) {
@@ -3593,8 +3596,7 @@ __global__ __launch_bounds__(256) void k_wide_l1s(const WideArgs a) {
 #pragma unroll
         for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(dt * dt, self[q], tot[s][q]);
       } else {
-        const int cnt = __builtin_amdgcn_readlane(cnt_l, s);
-        const float inv = ((mv >> s) & 1u) ? 1.f / static_cast<float>(max(cnt + sm, 1)) : 0.f;
+        const float inv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(inv_l), s));
 #pragma unroll
         for (int q = 0; q < FPL; ++q) tot[s][q] = fmaf(static_cast<float>(sm), self[q], tot[s][q]) * inv;
       }
