@@ -5384,6 +5384,13 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const bool l1s_k = k1 == k_wide_l1s<1, true> || k1 == k_wide_l1s<1, false> || k1 == k_wide_l1s<2, true> ||
                      k1 == k_wide_l1s<2, false> || k1 == k_wide_l1s<4, true> || k1 == k_wide_l1s<4, false>;
   if (ws2 && l1s_k && !(cte && std::strcmp(cte, "0") == 0)) a1.ctab = a2.ctab = reinterpret_cast<float*>(ws + W.ct);
+  // kept in-degrees (k_wide_degree) are read by GCN terms and by k_wide_l1m's MEAN counts; the
+  // default k_wide_l1s and the layer-2 kernels count a MEAN term's kept edges themselves (SAGE:
+  // no degree pass, 0.37 ms per c3 pass)
+  bool any_gcn = false;
+  for (int l = 0; l < 2; ++l)
+    for (int k = 0; k < p->layers[l].n_terms; ++k) any_gcn |= p->layers[l].terms[k].kind == XPG_TERM_GCN;
+  const bool need_kin = W.gcn && (any_gcn || !l1s_k);
   const size_t lds2 = ws2 ? lds_ws + (idx ? sizeof(int) * 3 * kIxInts : 0) + (th ? sizeof(float) * 2 * l2.f_out_pad : 0)
                           : W.lds;
   const char* gwe0 = getenv("XPG_WIDE_GW");
@@ -5416,7 +5423,7 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
                        p->n0, mT0);
     XPG_LAUNCHED();
     prof_end(st, XPG_PROF_WIDE_F0);
-    if (W.gcn) {
+    if (need_kin) {
       const int64_t n = (int64_t)p->n_rel * p->n0 * 32;
       prof_begin(st, XPG_PROF_WIDE_DEGREE);
       hipLaunchKernelGGL(k_wide_degree, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, st, mT, mT0, p->n0,
