@@ -2584,7 +2584,10 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       ix[kIxOrder + lane] = lane < na ? nth_set_bit(qc_mv, lane) : nth_set_bit(~qc_mv, lane - na);
     }
   };
-  const bool ixw = IDX && wave == GW && !(a.dbg & 32);  // the index wave (MFMA wave 0)
+  // the index wave: the last MFMA wave (MFMA wave 0 also writes the logits; per-wave stamps,
+  // profiles/r4_ws_stamps_*.log: the MFMA waves past the first wait at the barrier for about half
+  // of each interval)
+  const bool ixw = IDX && wave == GW + 3 && !(a.dbg & 32);
   // TH (with IDX): the layer bias and the head's weight row in LDS after the lists ([f_out_pad]
   // each), read back four columns at a time by the transposed epilogue
   float* const HBW = reinterpret_cast<float*>(IX + 3 * kIxInts);

@@ -60,7 +60,7 @@ def main():
         for w in range(12):
             v = buf[:nwg, w, :].astype(np.float64).mean(axis=0) / ntgt
             names = GATHER if w < 8 else MFMA
-            role = f"gather w{w}" if w < 8 else ("index+mfma w8" if w == 8 else f"mfma w{w}")
+            role = f"gather w{w}" if w < 8 else ("logit+mfma w8" if w == 8 else ("index+mfma w11" if w == 11 else f"mfma w{w}"))
             cells = "  ".join(f"{n} {v[k]:7.0f}" for k, n in enumerate(names))
             print(f"  {role:14s} total {v.sum():7.0f} | {cells}", flush=True)
     set_env("")
