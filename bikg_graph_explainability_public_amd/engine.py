@@ -637,7 +637,9 @@ def _workspace(dev, nbytes):
     key = (dev.type, dev.index)
     t = _WS.get(key)
     if t is None or t.numel() < nbytes:
-        t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        # grown to the next power of two (>= 1 MiB): queries of other sizes reuse it instead of
+        # each first call on a larger one paying a device allocation
+        t = torch.empty(max(1 << 20, 1 << (max(nbytes, 1) - 1).bit_length()), dtype=torch.uint8, device=dev)
         _WS[key] = t
     return t
 
