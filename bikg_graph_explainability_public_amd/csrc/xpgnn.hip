@@ -16,6 +16,8 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <mutex>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/xpgnn.h"
@@ -37,6 +39,24 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 #define XPG_LAUNCHED() XPG_HIP(hipGetLastError())
+
+// A kernel's dynamic-LDS limit is raised once, to all the CU's LDS its static LDS leaves (a launch
+// still reserves only the bytes it asks for).  Set per launch to a new plan's size, the attribute
+// call cost ~6 ms of host time in the HIP runtime on every new plan size (k_rows_forward,
+// k_wlm_fit_mc: profiles/r4_api_first_calls.log).
+hipError_t lds_limit(const void* f) {
+  static std::mutex mu;
+  static std::unordered_set<const void*> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count(f)) return hipSuccess;
+  hipFuncAttributes fa;
+  hipError_t e = hipFuncGetAttributes(&fa, f);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          160 * 1024 - static_cast<int>(fa.sharedSizeBytes));
+  if (e == hipSuccess) done.insert(f);
+  return e;
+}
 
 // Diagnostics switches (ablations that change results: XPG_WIDE_DBG, XPG_L1_DBG) are honoured
 // only together with XPG_DIAGNOSTICS=1; set without it they are an error, so a variable leaked
@@ -5090,8 +5110,7 @@ int try_fused_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t r
   const int64_t grid = std::min<int64_t>(cdiv(rows, wpb), 256 * per_cu);
 #define XPG_FUSED(W)                                                                                     \
   if (wpb == W) {                                                                                        \
-    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_forward<W>),                       \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));       \
+    XPG_HIP(lds_limit(reinterpret_cast<const void*>(&k_fused_forward<W>)));       \
     hipLaunchKernelGGL(k_fused_forward<W>, dim3(static_cast<unsigned>(grid)), dim3(W * 64), lds, st, a); \
     XPG_LAUNCHED();                                                                                      \
     return XPG_OK;                                                                                       \
@@ -5401,10 +5420,8 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   const bool l1m = k1 == k_wide_l1m;
   const size_t lds1 = l1m ? sizeof(float) * 32 * (size_t)(l1.f_out_pad + 4) : sizeof(float) * 3 * kWideCap;
   const int thr1 = l1m ? 512 : 256;
-  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds1)));
-  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              static_cast<int>(lds2)));
+  XPG_HIP(lds_limit(reinterpret_cast<const void*>(k1)));
+  XPG_HIP(lds_limit(reinterpret_cast<const void*>(k2)));
   const int cus = device_cus();
   // persistent grids sized to residency (static target striding: no late starters)
   int per_cu1 = 0, per_cu2 = 0;
@@ -5578,8 +5595,7 @@ int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t ro
   const dim3 grid(static_cast<unsigned>(cdiv(rows, 64)));
 #define XPG_ROWS(F)                                                                                     \
   if (fs == F) {                                                                                        \
-    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rows_forward<F>),                       \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)));      \
+    XPG_HIP(lds_limit(reinterpret_cast<const void*>(&k_rows_forward<F>)));      \
     hipLaunchKernelGGL(k_rows_forward<F>, grid, dim3(64 * kRowsWaves), lds, st, a);                      \
     XPG_LAUNCHED();                                                                                     \
     return XPG_OK;                                                                                      \
@@ -6161,8 +6177,7 @@ static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib, P,
                      step0, stp, nullptr, int64_t(0), nullptr, 0);
   XPG_LAUNCHED();
-  XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gw_grad),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_g)));
+  XPG_HIP(lds_limit(reinterpret_cast<const void*>(&k_gw_grad)));
   const dim3 gw(static_cast<unsigned>(L.n_wg), nf);
   for (int64_t t = 0; t < steps; ++t) {
     hipLaunchKernelGGL(k_gw_p, gw, dim3(kGpWaves * 64), 0, st, bits, rows, cols, words, ib, t, w, p_part);
@@ -6351,8 +6366,7 @@ static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, in
     const dim3 grid(static_cast<unsigned>(L.xcd ? 8 * L.P * cdiv(n_fits, 8) : n_fits * L.P));
 #define XPG_WLM_MC(C, G)                                                                                    \
     if (!launched && L.mc_cpl == C && L.mc_stg == G) {                                                      \
-      XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit_mc<C, G>),                       \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds_mc))); \
+      XPG_HIP(lds_limit(reinterpret_cast<const void*>(&k_wlm_fit_mc<C, G>))); \
       hipLaunchKernelGGL((k_wlm_fit_mc<C, G>), grid, dim3(1024), L.lds_mc, st, bits, colbits, rows, ic, words, ib, \
                          L.bw, L.P, L.wpp, L.mc_ds, n_fits, L.xcd ? 1 : 0, kernel, stp, *params, w, adam_m,      \
                          adam_v, p_hist, w_hist, xp, cnt + n_fits, spin, fault, epoch, plain_ok,             \
@@ -6372,8 +6386,7 @@ static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, in
   const int cpt = static_cast<int>(cdiv(cols, 1024));
 #define XPG_WLM(C, TL)                                                                                     \
   if (!launched && cpt <= C && L.stage == TL) {                                                                      \
-    XPG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wlm_fit<C, TL>),                          \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(L.lds)));     \
+    XPG_HIP(lds_limit(reinterpret_cast<const void*>(&k_wlm_fit<C, TL>)));     \
     hipLaunchKernelGGL((k_wlm_fit<C, TL>), dim3(nf), dim3(1024), L.lds, st, bits, colbits, rows, ic, words, \
                        ib, L.bw, L.n_bs, L.n_ds, kernel, stp, *params, w, adam_m, adam_v, p_hist, w_hist,  \
                        t_glob);                                                                            \

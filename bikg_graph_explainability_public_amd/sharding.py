@@ -154,6 +154,19 @@ def gather_map(n, fn, group=None):
     return gather_rows(fn(s, e), n, group)
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    """One side stream per device, reused by every call: torch.cuda.Stream() hands out the next
+    stream of torch's pool, and the first work on each new HIP stream pays its hardware-queue
+    setup (~6 ms per call on the first new streams: profiles/r4_api_first_calls.log)."""
+    key = (device.type, device.index)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
 def gather_map_beside(n, fn, side_fn, group=None):
     """`gather_map(n, fn)` with a second row-sharded job run beside it on a side stream.
 
@@ -167,7 +180,7 @@ def gather_map_beside(n, fn, side_fn, group=None):
     if not torch.cuda.is_available() or os.environ.get("XPG_SIDE_STREAM") == "0":
         return gather_rows(fn(s, e), n, group), gather_rows(side_fn(s, e), n, group)
     cur = torch.cuda.current_stream()
-    side = torch.cuda.Stream(device=cur.device)
+    side = _side_stream(cur.device)
     side.wait_stream(cur)  # the inputs (mask bits) are produced on the current stream
     main = fn(s, e)
     with torch.cuda.stream(side):
