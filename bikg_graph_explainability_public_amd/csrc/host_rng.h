@@ -12,8 +12,10 @@
 // and following bit 0 through it gives bit0 = y0 ^ y3 ^ y14 ^ y18 ^ y22 ^ y29, the parity of
 // y & 0x20444009 — no tempering per element, one AND + popcount.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <utility>
 #include <vector>
 #if !defined(__HIP_DEVICE_COMPILE__)
 #include <emmintrin.h>  // SSE2 (x86-64 baseline): host code only
@@ -108,6 +110,192 @@ inline void mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t row
       uint32_t v = static_cast<uint32_t>(two >> (off & 31));
       if (w == words - 1) v &= tail;
       o[w] = v;
+    }
+  }
+}
+
+// at::mt19937::operator(): one tempered 32-bit output (CPUGeneratorImpl::random())
+inline uint32_t next_u32(uint32_t* s, int32_t* left, int32_t* next) {
+  if (--*left == 0) {
+    next_state(s);
+    *left = kN;
+    *next = 0;
+  }
+  uint32_t y = s[(*next)++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+// torch.randperm(n) on the CPU generator (ATen randperm_cpu, n < 2^32 / 20): Fisher-Yates with
+// z = random() % (n - i), swapping positions i and i + z, for i = 0 .. n - 2.
+inline void randperm(uint32_t* s, int32_t* left, int32_t* next, int64_t n, std::vector<int64_t>* out) {
+  out->resize(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; ++i) (*out)[i] = i;
+  for (int64_t i = 0; i + 1 < n; ++i) {
+    const int64_t z = static_cast<int64_t>(next_u32(s, left, next)) % (n - i);
+    std::swap((*out)[i], (*out)[i + z]);
+  }
+}
+
+inline bool stream_bit(const std::vector<uint32_t>& st, int64_t i) { return (st[i >> 5] >> (i & 31)) & 1u; }
+
+// `nb` (<= 32) stream bits from bit position i, LSB first (the stream has 2 words of slack)
+inline uint32_t stream_bits(const uint32_t* st, int64_t i, int nb) {
+  const uint64_t two = static_cast<uint64_t>(st[i >> 5]) | (static_cast<uint64_t>(st[(i >> 5) + 1]) << 32);
+  const uint32_t v = static_cast<uint32_t>(two >> (i & 31));
+  return nb >= 32 ? v : v & ((1u << nb) - 1u);
+}
+
+// The compat community mask rows of Mask.mask_generator (reference masks.py:299-348 with
+// get_internal_mask masks.py:81-136, get_external_indices masks.py:138-194 and Pathways'
+// mask_generator / activate_dead_mask / pathway_mask2node_mask, pathways.py:234-385), drawn from
+// torch's CPU generator in the reference's call order, written UNSHUFFLED as bit-packed rows
+// out[rows][words] (zeroed by the caller).  Per block {row_start, size, size_internal, own, e}
+// in length-descending community order:
+//   internal = randint(0, 2, (size, |own|), bool)                    masks.py:130
+//   pm = randint(0, 2, (half, n), bool), then ~pm, then (if size - size_internal is odd) one
+//        more randint(0, 2, (1, n), bool) row; half = (size - size_internal) // 2  pathways.py:260-281
+//   pm[:, e] = False  (the reference switches off column e, the block's position in sorted
+//        order, not the block's own community)                         masks.py:178
+//   n > 1 and pm all False: order = randperm(n) without e, row r switches on order[r % (n-1)]
+//                                                                      pathways.py:318-333
+//   rows size_internal.. of the block: OR of the members of every community pm switches on
+//   every row of the block: column own[j] := internal[r][j], j ascending (members sorted)
+// comm_ptr / comm_cols: CSR of every community's member columns (ascending), n communities.
+//
+// The external OR runs over tables of the member masks of groups of g communities (all 2^g
+// unions per group, g chosen so the tables stay <= 4 M words): a row ORs ceil(n / g) table rows
+// instead of one member mask per switched-on community.  The internal assignment clears the
+// own community's columns and sets the drawn ones (a community listing a column twice keeps
+// the sequential last-write semantics instead).
+inline void community_rows(uint32_t* s, int32_t* left, int32_t* next, int64_t cols, int32_t n,
+                           const int32_t* comm_ptr, const int32_t* comm_cols, const int32_t* blocks,
+                           int32_t n_blocks, uint32_t* out) {
+  const int64_t words = (cols + 31) / 32;
+  int g = 8;
+  while (g > 1 && ((n + g - 1) / g) * (int64_t(1) << g) * words > (int64_t(4) << 20)) --g;
+  const int groups = (n + g - 1) / g;
+  // member masks per community (also the own-column clear masks of the internal assignment)
+  std::vector<uint32_t> cmask(static_cast<size_t>(n) * words, 0u);
+  std::vector<uint8_t> dup(n, 0);
+  for (int c = 0; c < n; ++c)
+    for (int64_t k = comm_ptr[c]; k < comm_ptr[c + 1]; ++k) {
+      cmask[c * words + (comm_cols[k] >> 5)] |= 1u << (comm_cols[k] & 31);
+      if (k > comm_ptr[c] && comm_cols[k] == comm_cols[k - 1]) dup[c] = 1;
+    }
+  const bool tables = (int64_t)groups * (int64_t(1) << g) * words <= (int64_t(4) << 20);
+  std::vector<uint32_t> tab;
+  if (tables) {
+    tab.assign(static_cast<size_t>(groups) * (size_t(1) << g) * words, 0u);
+    for (int G = 0; G < groups; ++G) {
+      uint32_t* tg = tab.data() + static_cast<size_t>(G) * (size_t(1) << g) * words;
+      for (uint32_t code = 1; code < (1u << g); ++code) {
+        const int low = __builtin_ctz(code), c = G * g + low;
+        const uint32_t* prev = tg + static_cast<size_t>(code & (code - 1)) * words;
+        uint32_t* dst = tg + static_cast<size_t>(code) * words;
+        if (c < n) {
+          const uint32_t* m = cmask.data() + static_cast<size_t>(c) * words;
+          for (int64_t w = 0; w < words; ++w) dst[w] = prev[w] | m[w];
+        } else {
+          for (int64_t w = 0; w < words; ++w) dst[w] = prev[w];
+        }
+      }
+    }
+  }
+  const int pmw = (n + 31) / 32;  // words of one community-flag row
+  std::vector<uint32_t> st_int, st_ext, st_extra, pm;
+  std::vector<int64_t> perm;
+  for (int b = 0; b < n_blocks; ++b) {
+    const int64_t start = blocks[5 * b], size = blocks[5 * b + 1], si = blocks[5 * b + 2];
+    const int own = blocks[5 * b + 3], e = blocks[5 * b + 4];
+    const int64_t o0 = comm_ptr[own], len = comm_ptr[own + 1] - o0;
+    auto draw = [&](int64_t count, std::vector<uint32_t>* st) {
+      st->assign(static_cast<size_t>((count + 31) / 32 + 2), 0u);
+      if (count > 0) lsb_stream(s, left, next, count, st->data());
+    };
+    draw(size * len, &st_int);
+    const int64_t ext = size - si, half = ext / 2;
+    draw(half * n, &st_ext);
+    const bool extra = (ext % 2) != 0;
+    if (extra) draw(n, &st_extra);
+    // community flags per external row, packed: drawn rows, their complements, the extra row
+    pm.assign(static_cast<size_t>(ext * pmw), 0u);
+    const uint32_t emask = ~(1u << (e & 31));
+    bool any = false;
+    for (int64_t r = 0; r < ext; ++r) {
+      uint32_t* f = pm.data() + r * pmw;
+      const uint32_t* src = r < 2 * half ? st_ext.data() : st_extra.data();
+      const int64_t base = r < half ? r * n : r < 2 * half ? (r - half) * n : 0;
+      const bool flip = r >= half && r < 2 * half;
+      for (int w = 0; w < pmw; ++w) {
+        const int nb = std::min(32, n - 32 * w);
+        uint32_t v = stream_bits(src, base + 32 * w, nb);
+        if (flip) v = ~v & (nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u));
+        if (w == (e >> 5)) v &= emask;
+        f[w] = v;
+        any = any || v != 0u;
+      }
+    }
+    if (n - 1 > 0 && !any) {
+      randperm(s, left, next, n, &perm);
+      std::vector<int64_t> order;
+      for (int64_t v : perm)
+        if (v != e) order.push_back(v);
+      if (!order.empty())
+        for (int64_t r = 0; r < ext; ++r) {
+          const int64_t c = order[r % static_cast<int64_t>(order.size())];
+          pm[r * pmw + (c >> 5)] |= 1u << (c & 31);
+        }
+    }
+    for (int64_t r = 0; r < ext; ++r) {
+      uint32_t* __restrict__ row = out + (start + si + r) * words;
+      const uint32_t* f = pm.data() + r * pmw;
+      if (tables) {
+        for (int G = 0; G < groups; ++G) {
+          const int bit = G * g;
+          const uint64_t two = static_cast<uint64_t>(f[bit >> 5]) |
+                               ((bit >> 5) + 1 < pmw ? static_cast<uint64_t>(f[(bit >> 5) + 1]) << 32 : 0ull);
+          const uint32_t code = static_cast<uint32_t>(two >> (bit & 31)) & ((1u << g) - 1u);
+          if (!code) continue;
+          const uint32_t* __restrict__ t = tab.data() + (static_cast<size_t>(G) << g | code) * words;
+          for (int64_t w = 0; w < words; ++w) row[w] |= t[w];
+        }
+      } else {
+        for (int c = 0; c < n; ++c)
+          if ((f[c >> 5] >> (c & 31)) & 1u)
+            for (int64_t k = comm_ptr[c]; k < comm_ptr[c + 1]; ++k)
+              row[comm_cols[k] >> 5] |= 1u << (comm_cols[k] & 31);
+      }
+    }
+    const int32_t* oc = comm_cols + o0;
+    if (!dup[own]) {
+      const uint32_t* om = cmask.data() + static_cast<size_t>(own) * words;
+      const int64_t wlo = len ? oc[0] >> 5 : 0, whi = len ? oc[len - 1] >> 5 : -1;
+      for (int64_t r = 0; r < size; ++r) {
+        uint32_t* __restrict__ row = out + (start + r) * words;
+        for (int64_t w = wlo; w <= whi; ++w) row[w] &= ~om[w];
+        for (int64_t j0 = 0; j0 < len; j0 += 32) {
+          uint32_t v = stream_bits(st_int.data(), r * len + j0, static_cast<int>(std::min<int64_t>(32, len - j0)));
+          while (v) {
+            const int32_t col = oc[j0 + __builtin_ctz(v)];
+            row[col >> 5] |= 1u << (col & 31);
+            v &= v - 1u;
+          }
+        }
+      }
+    } else {
+      for (int64_t r = 0; r < size; ++r) {
+        uint32_t* row = out + (start + r) * words;
+        for (int64_t j = 0; j < len; ++j) {
+          const int32_t col = oc[j];
+          const uint32_t bit = 1u << (col & 31);
+          const uint32_t v = static_cast<uint32_t>(stream_bit(st_int, r * len + j));
+          row[col >> 5] = (row[col >> 5] & ~bit) | (v << (col & 31));
+        }
+      }
     }
   }
 }

@@ -5653,6 +5653,36 @@ int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t
   return XPG_OK;
 }
 
+int xpg_mt19937_community_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t cols, int32_t n_comm,
+                               const int32_t* comm_ptr, const int32_t* comm_cols, const int32_t* blocks,
+                               int32_t n_blocks, int64_t rows, uint32_t* bits) {
+  XPG_REQ(state && left && next && comm_ptr && blocks && bits && cols > 0 && n_comm > 0 && n_blocks > 0 &&
+              n_blocks <= n_comm && rows > 0,
+          "mt19937_community_bits: bad arguments");
+  const bool fresh = *left == 1 && *next == 0;
+  XPG_REQ(fresh || (*left >= 1 && *next >= 0 && *next + *left - 1 == hostrng::kN),
+          "mt19937_community_bits: generator position (left, next) is not an at::mt19937 state");
+  XPG_REQ(comm_ptr[0] == 0, "mt19937_community_bits: comm_ptr[0] != 0");
+  for (int32_t c = 0; c < n_comm; ++c) {
+    XPG_REQ(comm_ptr[c + 1] >= comm_ptr[c], "mt19937_community_bits: comm_ptr not monotone");
+    for (int32_t k = comm_ptr[c]; k < comm_ptr[c + 1]; ++k) {
+      XPG_REQ(comm_cols[k] >= 0 && comm_cols[k] < cols, "mt19937_community_bits: member column out of range");
+      XPG_REQ(k == comm_ptr[c] || comm_cols[k] >= comm_cols[k - 1], "mt19937_community_bits: members not sorted");
+    }
+  }
+  int64_t end = 0;
+  for (int32_t b = 0; b < n_blocks; ++b) {
+    const int32_t* q = blocks + 5 * b;
+    XPG_REQ(q[0] == end && q[1] >= 1 && q[2] >= 1 && q[2] <= q[1] && q[3] >= 0 && q[3] < n_comm && q[4] == b,
+            "mt19937_community_bits: blocks must be {row_start, size, size_internal, own, b} back to back");
+    end += q[1];
+  }
+  XPG_REQ(end == rows, "mt19937_community_bits: rows != the blocks' total");
+  std::memset(bits, 0, sizeof(uint32_t) * static_cast<size_t>(rows) * static_cast<size_t>(words_of(cols)));
+  hostrng::community_rows(state, left, next, cols, n_comm, comm_ptr, comm_cols, blocks, n_blocks, bits);
+  return XPG_OK;
+}
+
 #ifdef XPG_WIDE_STAMPS  // diagnostic build only: layer-2 phase cycles [512 workgroups][16 waves][8]
 int xpg_debug_wide_stamps(uint64_t* out) {
   XPG_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wide_stamps), sizeof(uint64_t) * 512 * 16 * 8));

@@ -140,8 +140,10 @@ class Data:
         return torch.cat(mapped, dim=1), torch.cat(types), pointers
 
     # -------------------------------------------------------------- computational graph
-    def comp_graph(self, ind, n_hops, problem, names, node_types=None, edge_types=None):
-        """data.py:281-361 — k-hop computational subgraph with one hop more than the model."""
+    def comp_graph(self, ind, n_hops, problem, names, node_types=None, edge_types=None,
+                   return_pos=False):
+        """data.py:281-361 — k-hop computational subgraph with one hop more than the model.
+        `return_pos` appends the positions of `sub_names` in `names` (int64 numpy array)."""
         hops = n_hops + 1
         n = self.feat.shape[0]
         subset, sub_ei, sub_ind, emask = k_hop_subgraph(ind, hops, self.edge_index, n)
@@ -154,10 +156,13 @@ class Data:
         pos = subset if "node" in problem or "graph" in problem else torch.where(emask)[0]
         # the reference indexes np.array(names, dtype=str) (data.py:341-356); only the subgraph's
         # names are converted here, not every name of the graph (1M of them at c3)
-        sub_names = take_names(names, pos.cpu().numpy())
+        pos = pos.cpu().numpy()
+        sub_names = take_names(names, pos)
+        if return_pos:
+            return sub_feat, sub_ei, sub_names, sub_ind, sub_nt, sub_et, pos
         return sub_feat, sub_ei, sub_names, sub_ind, sub_nt, sub_et
 
-    def edge_comp_graph(self, ind, n_hops, names):
+    def edge_comp_graph(self, ind, n_hops, names, return_pos=False):
         """Computational graph of an edge problem (edge masks mode; the reference's data.py:281-361
         hands the edge index to k_hop_subgraph as a node id, so its edge path is broken): nodes
         within n_hops + 1 hops of either endpoint of edge `ind`, every edge with both ends inside
@@ -179,9 +184,11 @@ class Data:
         keep = node[ei[0]] & node[ei[1]]
         pos = torch.nonzero(keep).reshape(-1)
         sub_ind = int(torch.nonzero(pos == int(ind)).reshape(-1)[0])
-        sub_names = take_names(names, pos.cpu().numpy())
-        return (self.feat[subset], remap[ei[:, keep]], sub_names, sub_ind,
-                (int(remap[u]), int(remap[v])))
+        pos = pos.cpu().numpy()
+        sub_names = take_names(names, pos)
+        out = (self.feat[subset], remap[ei[:, keep]], sub_names, sub_ind,
+               (int(remap[u]), int(remap[v])))
+        return out + (pos,) if return_pos else out
 
     def element_size(self, problem):
         """data.py:363-388."""

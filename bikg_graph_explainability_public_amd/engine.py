@@ -14,6 +14,7 @@ import contextlib
 import ctypes
 import os
 import gc
+import itertools
 import math
 
 import numpy as np
@@ -100,19 +101,57 @@ def compat_shapley_bits(rows: int, cols: int):
     memory (pinned when a GPU is present), with the generator advanced past the draw exactly as
     torch would advance it: the library replays the generator's MT19937 state natively
     (xpg_mt19937_mask_bits, host code), without the [rows, cols] bool tensor."""
-    raw = torch.get_rng_state().numpy().copy()
-    left = raw[_RNG_LEFT:_RNG_LEFT + 4].view(np.int32).copy()
-    nxt = np.array([int(raw[_RNG_NEXT:_RNG_NEXT + 8].view(np.uint64)[0])], dtype=np.int32)
-    state = raw[_RNG_STATE:_RNG_STATE + 624 * 8].view(np.uint64).astype(np.uint32)
+    raw, state, left, nxt = _rng_get()
     out = torch.empty((rows, words_of(cols)), dtype=torch.int32,
                       pin_memory=torch.cuda.is_available())
     call("xpg_mt19937_mask_bits", state.ctypes.data, left.ctypes.data, nxt.ctypes.data, int(rows),
          int(cols), out.data_ptr() if rows else None)
+    _rng_set(raw, state, left, nxt)
+    return out
+
+
+def compat_community_bits(cols: int, communities, blocks):
+    """The reference's compat community draws (Mask.mask_generator with communities,
+    masks.py:299-348 + pathways.py:234-385) on torch's global CPU generator, bit-identical, as
+    UNSHUFFLED bit-packed int32 [rows, ceil(cols / 32)] host rows (pinned when a GPU is
+    present); the generator is advanced exactly as the reference's torch calls advance it, so
+    the caller's row shuffle (torch.randperm) follows on the same stream.  `communities`: every
+    community's member columns (each sorted ascending, as the reference sorts them in place);
+    `blocks`: int32 [n_blocks, 5] {row_start, size, size_internal, own, b} (Mask.community_plan).
+    Host code in the library (xpg_mt19937_community_bits)."""
+    blocks = np.ascontiguousarray(np.asarray(blocks), dtype=np.int32).reshape(-1, 5)
+    lens = np.fromiter((len(c) for c in communities), dtype=np.int64, count=len(communities))
+    ptr_ = np.zeros(lens.size + 1, dtype=np.int32)
+    np.cumsum(lens, out=ptr_[1:])
+    flat = np.fromiter(itertools.chain.from_iterable(communities), dtype=np.int64,
+                       count=int(lens.sum()))
+    flat = np.ascontiguousarray(flat if flat.size else np.zeros(1, np.int64), dtype=np.int32)
+    rows = int(blocks[-1, 0]) + int(blocks[-1, 1])
+    out = torch.empty((rows, words_of(cols)), dtype=torch.int32,
+                      pin_memory=torch.cuda.is_available())
+    raw, state, left, nxt = _rng_get()
+    call("xpg_mt19937_community_bits", state.ctypes.data, left.ctypes.data, nxt.ctypes.data,
+         int(cols), int(lens.size), ptr_.ctypes.data, flat.ctypes.data, blocks.ctypes.data,
+         int(blocks.shape[0]), rows, out.data_ptr())
+    _rng_set(raw, state, left, nxt)
+    return out
+
+
+def _rng_get():
+    """torch's CPU generator state as (raw bytes, state[624] uint32, left int32[1], next int32[1])."""
+    raw = torch.get_rng_state().numpy().copy()
+    left = raw[_RNG_LEFT:_RNG_LEFT + 4].view(np.int32).copy()
+    nxt = np.array([int(raw[_RNG_NEXT:_RNG_NEXT + 8].view(np.uint64)[0])], dtype=np.int32)
+    state = raw[_RNG_STATE:_RNG_STATE + 624 * 8].view(np.uint64).astype(np.uint32)
+    return raw, state, left, nxt
+
+
+def _rng_set(raw, state, left, nxt):
+    """Write an advanced (state, left, next) back into torch's CPU generator."""
     raw[_RNG_LEFT:_RNG_LEFT + 4] = left.view(np.uint8)
     raw[_RNG_NEXT:_RNG_NEXT + 8] = np.array([nxt[0]], dtype=np.uint64).view(np.uint8)
     raw[_RNG_STATE:_RNG_STATE + 624 * 8] = state.astype(np.uint64).view(np.uint8)
     torch.set_rng_state(torch.from_numpy(raw))
-    return out
 
 
 def sample_shapley_dev(seed: torch.Tensor, rows: int, cols: int, row_offset: int = 0,
@@ -592,6 +631,11 @@ class ForwardPlan:
             setattr(obj, field, base + 4 * int(o))
         self._staged = []
 
+    def device_bytes(self):
+        """Device memory the plan holds: its arrays, tables, weights and forward workspace."""
+        held = self._keep + ([self._ws] if self._ws is not None else [])
+        return sum(t.numel() * t.element_size() for t in held)
+
     def workspace_bytes(self, rows):
         n = ctypes.c_size_t(0)
         _lib.check(_lib.load().xpg_forward_workspace(ctypes.byref(self.desc), rows, ctypes.byref(n)))
@@ -637,9 +681,16 @@ def _workspace(dev, nbytes):
     key = (dev.type, dev.index)
     t = _WS.get(key)
     if t is None or t.numel() < nbytes:
-        # grown to the next power of two (>= 1 MiB): queries of other sizes reuse it instead of
-        # each first call on a larger one paying a device allocation
-        t = torch.empty(max(1 << 20, 1 << (max(nbytes, 1) - 1).bit_length()), dtype=torch.uint8, device=dev)
+        # grown with 25 % headroom, in whole MiB (>= 4 MiB): queries of somewhat larger sizes
+        # reuse it instead of each first call on a larger one paying a device allocation; an
+        # allocation the headroom does not fit falls back to the exact size
+        _WS.pop(key, None)
+        del t
+        grow = max(4 << 20, (nbytes + nbytes // 4 + (1 << 20) - 1) >> 20 << 20)
+        try:
+            t = torch.empty(grow, dtype=torch.uint8, device=dev)
+        except torch.OutOfMemoryError:
+            t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
         _WS[key] = t
     return t
 

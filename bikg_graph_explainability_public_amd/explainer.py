@@ -13,6 +13,7 @@ reference's order (compat sampler), so results match the reference CPU path for 
 import random
 import time
 import warnings
+import weakref
 
 import numpy as np
 import torch
@@ -175,28 +176,69 @@ class Explainer:
                 tuple(getattr(plan, "lowering", ())))
 
     def _query_key(self, element, device):
-        """What prepare() and the query's ForwardPlan depend on: the element and problem, the
-        graph (every tensor's storage, in-place version and shape), the names / pathways /
-        type inputs (identity plus a cheap content fingerprint), the module state (parameter
-        storage and version counters) and the arch-check mode.  prepare() draws no random
-        numbers, so reusing its result leaves every RNG stream as the reference's."""
-        def ts(x):
-            if isinstance(x, dict):
-                return tuple((k, ts(v)) for k, v in x.items())
-            if isinstance(x, torch.Tensor):
-                return (x.data_ptr(), x._version, tuple(x.shape))
-            if isinstance(x, (list, tuple)):
-                n = len(x)
-                return (id(x), n) + tuple(str(x[i]) if not isinstance(x[i], (list, tuple))
-                                          else (len(x[i]),) + tuple(map(str, x[i][:1] + x[i][-1:]))
-                                          for i in (0, n // 2, n - 1) if n)
-            return id(x)
-        state = tuple((t.data_ptr(), t._version) for t in self.arch.parameters())
-        bufs = tuple((t.data_ptr(), t._version) for t in self.arch.buffers())
+        """The cache slot of a query: element, problem, device and modes.  Whether the slot's
+        entry still holds for the current inputs is `_query_sources` + `_query_content_ok`'s
+        business (prepare() draws no random numbers, so reusing its result leaves every RNG
+        stream as the reference's)."""
         return (str(element), type(element).__name__, self.problem, self.edge_masks, str(device),
-                ts(self.feat), ts(self.edge_index), ts(self.names), ts(self.pathways),
-                ts(self.pathway_names), ts(self.node_types), ts(self.edge_types), self.element_type,
-                id(self.arch), state, bufs, str(self.params.get("verify_arch", True)))
+                _freeze(self.element_type), str(self.params.get("verify_arch", True)))
+
+    def _query_sources(self):
+        """Identity snapshot of what prepare() and the query's ForwardPlan read: the graph and
+        type tensors (weak reference + storage + in-place version: a replaced tensor, even one
+        the allocator put at the freed address, or an in-place edit never matches), the names /
+        pathways inputs and the module (identity), the module's parameters and buffers."""
+        return _snapshot((self.feat, self.edge_index, self.node_types, self.edge_types,
+                          self.names, self.pathways, self.pathway_names, self.arch,
+                          tuple(self.arch.parameters()), tuple(self.arch.buffers())))
+
+    def _query_fingerprints(self):
+        """Full-content fingerprints of the inputs read in full by prepare(): pathways and
+        their names (community filtering), and hetero (dict) names."""
+        return (_content_fp(self.pathways), _content_fp(self.pathway_names),
+                _content_fp(self.names) if isinstance(self.names, dict) else None)
+
+    def _query_content_ok(self, element, entry):
+        """A cached entry's inputs are the same objects; check that their content did not change
+        in place where prepare() read it: the pathways in full, the element's position in the
+        names and the subgraph's names at their positions (O(S), not O(N))."""
+        if entry["fp"] != self._query_fingerprints():
+            return False
+        c = entry["c"]
+        if isinstance(self.names, dict) or c["ind"] is None:
+            return True
+        try:
+            if self.extract_index(element, self.names) != c["ind"]:
+                return False
+        except AssertionError:
+            return False
+        if c["pos"] is not None:
+            from .data import take_names
+            return take_names(self.names, c["pos"]) == c["sub_names"]
+        return True
+
+    def clear_cache(self):
+        """Drop every cached query (computational subgraph, plan and its device buffers)."""
+        self._queries.clear()
+
+    def _trim_cache(self, keep):
+        """Keep the cache within params["plan_cache_bytes"] device bytes (default 2 GiB) and
+        8 queries: oldest entries out first; the entry of the query just run always stays."""
+        limit = int(self.params.get("plan_cache_bytes", 2 << 30))
+        user = _tensor_ptrs((self.feat, self.edge_index, self.node_types, self.edge_types))
+
+        def nbytes(e):
+            ctx = sum(t.numel() * t.element_size() for t in e["c"].values()
+                      if isinstance(t, torch.Tensor) and t.data_ptr() not in user)
+            return ctx + (e["plan"].device_bytes() if e["plan"] is not None else 0)
+        total = {k: nbytes(e) for k, e in self._queries.items()}
+        for k in list(self._queries):
+            if k == keep:
+                continue
+            if len(self._queries) <= 8 and sum(total.values()) <= limit:
+                break
+            del self._queries[k]
+            total.pop(k)
 
     # ------------------------------------------------------------------------------ run
     def prepare(self, element, device):
@@ -219,7 +261,7 @@ class Explainer:
         data = Data(feat, ei)
         sub_pw = sub_pw_names = None
         sub_nt = sub_et = None
-        link = None
+        link = pos = None
         if self.edge_masks:
             # edge problem, edge masks (non-compat: the reference's edge path is broken at
             # masks.py:294 and data.py:331): mask columns = the computational graph's edges
@@ -227,7 +269,8 @@ class Explainer:
                 raise NotImplementedError("edge masks: homogeneous graphs only")
             n_hops = Model(self.arch).get_hops(0)
             ind = self.extract_index(element, names)
-            sub_feat, sub_ei, sub_names, sub_ind, link = data.edge_comp_graph(ind, n_hops, names)
+            sub_feat, sub_ei, sub_names, sub_ind, link, pos = data.edge_comp_graph(
+                ind, n_hops, names, return_pos=True)
             if pathways is not None:
                 sub_pw, sub_pw_names, _ = Pathways(pathways, pathway_names,
                                                    pathway_types).comp_graph(sub_names)
@@ -235,16 +278,17 @@ class Explainer:
             rels = len(h_etypes) if h_etypes is not None else 0
             n_hops = Model(self.arch).get_hops(rels)
             ind = self.extract_index(element, names)
-            sub_feat, sub_ei, sub_names, sub_ind, sub_nt, sub_et = data.comp_graph(
-                ind, n_hops, self.problem, names, node_types, edge_types)
+            sub_feat, sub_ei, sub_names, sub_ind, sub_nt, sub_et, pos = data.comp_graph(
+                ind, n_hops, self.problem, names, node_types, edge_types, return_pos=True)
             if pathways is not None:
                 sub_pw, sub_pw_names, _ = Pathways(pathways, pathway_names,
                                                    pathway_types).comp_graph(sub_names)
         else:
-            sub_feat, sub_ei, sub_names = feat.clone(), ei.clone(), names
-            sub_ind = self.extract_index(element, sub_names)
-            sub_nt = node_types.clone() if node_types is not None else None
-            sub_et = edge_types.clone() if edge_types is not None else None
+            # the whole graph (explainer.py:427-447; the reference clones it, nothing here
+            # writes to it, so the run reads the caller's tensors and names directly)
+            sub_feat, sub_ei, sub_names = feat, ei, names
+            ind = sub_ind = self.extract_index(element, sub_names)
+            sub_nt, sub_et = node_types, edge_types
             if pathways is not None:
                 sub_pw, sub_pw_names = pathways, pathway_names
         if "graph" not in self.problem and not self.edge_masks and (self.element_type is not None or
@@ -266,7 +310,7 @@ class Explainer:
                 "sub_ind": sub_ind, "sub_nt": sub_nt, "sub_et": sub_et, "h_ntypes": h_ntypes,
                 "h_etypes": h_etypes, "padded_dims": padded_dims, "sub_pw": sub_pw,
                 "sub_pw_names": sub_pw_names, "sub_pw_inds": sub_pw_inds, "S": S,
-                "has_pathways": pathways is not None}
+                "has_pathways": pathways is not None, "ind": ind, "pos": pos}
 
     def run(self, element, times=1):
         """explainer.py:316-546."""
@@ -288,7 +332,15 @@ class Explainer:
         # subgraph, plan and arch check: prepare() and the plan build are the run's largest host
         # costs (explainer.py:345-480 redone by the reference on every call)
         qkey = self._query_key(element, device) if self.params.get("plan_cache", True) else None
-        cached = self._queries.get(qkey) if qkey is not None else None
+        entry = self._queries.get(qkey) if qkey is not None else None
+        cached = None
+        if entry is not None:
+            if _matches(self._query_sources(), entry["src"]) and \
+                    self._query_content_ok(element, entry):
+                cached = (entry["c"], entry["plan"], entry["arch_check"])
+            else:
+                del self._queries[qkey]  # stale: the inputs changed since it was prepared
+        hit = cached is not None
         c = cached[0] if cached else self.prepare(element, device)
         clock.mark("plan")
         sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
@@ -333,9 +385,10 @@ class Explainer:
             else:
                 arch_check = "cached"
         if qkey is not None:
-            if len(self._queries) >= 8 and qkey not in self._queries:
-                self._queries.pop(next(iter(self._queries)))  # oldest query out
-            self._queries[qkey] = (c, plan, arch_check)
+            self._queries.pop(qkey, None)  # (re)inserted as the newest entry
+            self._queries[qkey] = {"c": c, "plan": plan, "arch_check": arch_check,
+                                   "src": self._query_sources(),
+                                   "fp": entry["fp"] if hit else self._query_fingerprints()}
 
         clock.mark("sample")
         sampler = self.params.get("mask_sampler", "compat")
@@ -453,9 +506,12 @@ class Explainer:
             pathway_df = Pathways(c["sub_pw"], c["sub_pw_names"]).aggregate(mean,
                                                                             c["sub_pw_inds"])
         clock.mark("end")
+        if qkey is not None:
+            self._trim_cache(qkey)
         self.last_run = {"engine": plan is not None, "repeats": diag, "S": S,
                          "sub_ind": sub_ind, "plan": plan, "weights": config_vals,
-                         "phases": clock, "arch_check": arch_check}
+                         "phases": clock, "arch_check": arch_check,
+                         "query_cache": "off" if qkey is None else "hit" if hit else "miss"}
         return config_val_df, pathway_df
 
     def run_queries(self, elements, times=1):
@@ -579,12 +635,14 @@ _NAME_INDEX = {}
 
 
 def _name_index(names, element=None):
-    """(set(names), {str(name): first position}) of a names list — `element in names` and the
-    reference's np.where(np.array(names, dtype=str) == element)[0][0] as lookups — cached by
-    identity and length.  A hit is validated against the list itself (the cached position of
-    `element` must still hold it, and a name missing from the cached set is looked for again),
-    so a list edited in place is re-indexed instead of answering from a stale index; an edit
-    that adds an EARLIER copy of an indexed name at the same length is not detected."""
+    """(members, {str(name): first position}) of a names list — the reference's
+    `element in names` (members = set(names) of the names themselves, not their str forms: a
+    '5' is not a member of [5], as explainer.py:222 asserts) and its
+    np.where(np.array(names, dtype=str) == element)[0][0] as lookups — cached by identity and
+    length.  A hit is validated against the list itself (the cached position of `element` must
+    still hold it, and a name missing from the cached set is looked for again), so a list edited
+    in place is re-indexed instead of answering from a stale index; an edit that adds an EARLIER
+    copy of an indexed name at the same length is not detected."""
     key = (id(names), len(names))
     hit = _NAME_INDEX.get(key)
     if hit is not None and hit[0] is names:
@@ -600,10 +658,73 @@ def _name_index(names, element=None):
     idx = {}
     for i, n in enumerate(strs):
         idx.setdefault(n, i)
+    try:
+        members = set(names)
+    except TypeError:  # unhashable names: `element in names` on the list itself
+        members = names
     if len(_NAME_INDEX) > 8:
         _NAME_INDEX.clear()
-    _NAME_INDEX[key] = (names, set(strs), idx)
-    return _NAME_INDEX[key][1], idx
+    _NAME_INDEX[key] = (names, members, idx)
+    return members, idx
+
+
+def _snapshot(x):
+    """Identity snapshot of a run's input: tensors by weak reference + storage + in-place
+    version, tuples / dicts entry by entry (dict key order included), anything else (lists,
+    modules) by identity."""
+    if isinstance(x, torch.Tensor):
+        return ("t", weakref.ref(x), x.data_ptr(), x._version, tuple(x.shape))
+    if isinstance(x, tuple):
+        return ("u", tuple(_snapshot(v) for v in x))
+    if isinstance(x, dict):
+        return ("d", tuple(x.keys()), tuple(_snapshot(v) for v in x.values()))
+    return ("o", x)
+
+
+def _matches(a, b):
+    """Do two snapshots (`_snapshot`) name the same objects in the same state?"""
+    if a[0] != b[0]:
+        return False
+    if a[0] == "t":
+        return a[1]() is not None and a[1]() is b[1]() and a[2:] == b[2:]
+    if a[0] == "u":
+        return len(a[1]) == len(b[1]) and all(_matches(x, y) for x, y in zip(a[1], b[1]))
+    if a[0] == "d":
+        return a[1] == b[1] and all(_matches(x, y) for x, y in zip(a[2], b[2]))
+    return a[1] is b[1]
+
+
+def _freeze(x):
+    """Hashable, content-equal form of a nested list / tuple / dict of plain values."""
+    if isinstance(x, (list, tuple)):
+        return tuple(_freeze(v) for v in x)
+    if isinstance(x, dict):
+        return tuple((k, _freeze(v)) for k, v in x.items())
+    if isinstance(x, torch.Tensor):
+        return ("tensor", x.data_ptr(), x._version, tuple(x.shape))
+    return x
+
+
+def _content_fp(x):
+    """Full-content fingerprint of a names / pathways input (None stays None)."""
+    if x is None:
+        return None
+    f = _freeze(x)
+    try:
+        return (len(x), hash(f))
+    except TypeError:
+        return (len(x), repr(f))
+
+
+def _tensor_ptrs(xs):
+    """Storage pointers of the tensors in a nested tuple / dict of inputs."""
+    out = set()
+    for x in xs:
+        if isinstance(x, torch.Tensor):
+            out.add(x.data_ptr())
+        elif isinstance(x, dict):
+            out |= _tensor_ptrs(tuple(x.values()))
+    return out
 
 
 def _to_device(x, device):

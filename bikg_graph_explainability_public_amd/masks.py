@@ -17,6 +17,7 @@ Two samplers share one output contract (bool [R, S] rows + per-row community ind
 import itertools
 import math
 
+import numpy as np
 import torch
 from torch.utils.data import DataLoader
 
@@ -83,10 +84,20 @@ class Mask(Data):
         S = self.element_count()
         lens = torch.tensor([len(p) for p in self.pathways])
         order = torch.argsort(lens, descending=True)
+        # internal_sizes for every community at once, in the same float32 tensor arithmetic:
+        # `n / tensor` is Tensor.__rtruediv__ = reciprocal() * n (not a correctly rounded
+        # quotient), then ceil(fraction * total) and ceil(fraction * size), elementwise
+        frac = torch.sum(lens).reciprocal() * lens[order]
+        sizes = torch.ceil(frac * total)
+        sizes_int = torch.ceil(frac * sizes)
+        small = sizes_int < 3
+        sizes = torch.where(small, torch.full_like(sizes, 2), sizes).long().tolist()
+        sizes_int = torch.where(small, torch.ones_like(sizes_int), sizes_int).long().tolist()
+        order_l = order.tolist()
         blocks, start = [], 0
-        for e in range(order.shape[0]):
-            size, size_internal = self.internal_sizes(len(self.pathways[order[e]]), lens, total)
-            blocks.append((start, size, size_internal, int(order[e]), e))
+        for e in range(len(order_l)):
+            size, size_internal = sizes[e], sizes_int[e]
+            blocks.append((start, size, size_internal, order_l[e], e))
             start += size
             if start - size > total and S > 4000:
                 break
@@ -128,62 +139,92 @@ class Mask(Data):
         return self.feat.shape[0]
 
     def generate(self):
-        """Compat sampler: (mask bool [R, S] on CPU, pathway_rows int32 [R] or None)."""
+        """Compat sampler: (mask bool [R, S] on CPU, pathway_rows int32 [R] or None).
+        Community masks come from the native replay of the reference's draws
+        (`_community_bits`), unpacked; Shapley masks are the reference's torch.randint."""
         n_perturbs, epochs = self.assertions_mask_generator(self.params)
         total = n_perturbs * epochs
         S = self.element_count()
         if self.pathways is not None:
-            lens = torch.tensor([len(p) for p in self.pathways])
-            order = torch.argsort(lens, descending=True)
-            blocks, rows_of, sizes_of = [], [], []
-            cumulative = 0
-            for e in range(order.shape[0]):
-                pathway = self.pathways[order[e]]
-                pathway.sort()  # the reference sorts the caller's lists in place
-                internal, size_internal = self.get_internal_mask(pathway, lens, total, "cpu")
-                block = torch.zeros((internal.shape[0], S), dtype=torch.bool)
-                block = self.get_external_indices(block, e, size_internal)
-                block[:, pathway] = internal
-                rows_of.append([int(order[e])] * block.shape[0])
-                sizes_of.append([len(pathway)] * block.shape[0])
-                blocks.append(block)
-                if cumulative > total and S > 4000:
-                    break
-                cumulative += block.shape[0]
-            mask = torch.cat(blocks, dim=0)
-            prow = torch.tensor(list(itertools.chain.from_iterable(rows_of)), dtype=torch.int)
-            psize = torch.tensor(list(itertools.chain.from_iterable(sizes_of)), dtype=torch.int)
+            bits, prow = self._community_bits()
+            return _unpack_host(bits, S), prow
+        mask = self.shapley_mask((total, S), "cpu")
+        return mask[torch.randperm(mask.shape[0])], None
+
+    def _community_bits(self):
+        """The community compat draw as bit-packed host rows: (bits int32 [R, W], pathway_rows
+        int32 [R]).  The block plan (`community_plan`: the reference's per-community sizes,
+        length-descending order and early stop, masks.py:299-348) is built here; every random
+        draw of the block loop -- internal randint, antithetic external randint (+ extra row),
+        dead-mask randperm -- is replayed natively from torch's generator state
+        (engine.compat_community_bits); the row shuffle is torch.randperm on the advanced
+        generator, or the S > 4000 truncation to the rows of the largest communities
+        (masks.py:367-390).  Bit-identical to `_generate_torch` and the reference."""
+        from . import engine
+        n_perturbs, epochs = self.assertions_mask_generator(self.params)
+        total = n_perturbs * epochs
+        S = self.element_count()
+        blocks, src_rows, _, shuffle = self.community_plan()
+        for o in blocks[:, 3].tolist():
+            self.pathways[o].sort()  # the reference sorts the caller's lists in place
+        bits = engine.compat_community_bits(S, [sorted(p) for p in self.pathways], blocks)
+        # host bookkeeping in numpy (torch's threaded kernels cost more than they save here)
+        b = blocks.numpy()
+        prow = np.repeat(b[:, 3], b[:, 1]).astype(np.int32)
+        if shuffle:
+            ii = torch.randperm(src_rows).numpy()
         else:
-            mask = self.shapley_mask((total, S), "cpu")
-            prow = psize = None
-        if S > 4000 and mask.shape[0] > total and self.pathways is not None:
+            lens = torch.tensor([len(p) for p in self.pathways], dtype=torch.int)
+            ii = torch.argsort(lens[torch.from_numpy(prow).long()], descending=True)[:total].numpy()
+        return torch.from_numpy(bits.numpy()[ii]), torch.from_numpy(prow[ii])
+
+    def _generate_torch(self):
+        """The reference's community block loop (masks.py:299-390) in torch calls, draw for draw
+        (kept as the restatement the native replay `_community_bits` is tested against)."""
+        n_perturbs, epochs = self.assertions_mask_generator(self.params)
+        total = n_perturbs * epochs
+        S = self.element_count()
+        lens = torch.tensor([len(p) for p in self.pathways])
+        order = torch.argsort(lens, descending=True)
+        blocks, rows_of, sizes_of = [], [], []
+        cumulative = 0
+        for e in range(order.shape[0]):
+            pathway = self.pathways[order[e]]
+            pathway.sort()  # the reference sorts the caller's lists in place
+            internal, size_internal = self.get_internal_mask(pathway, lens, total, "cpu")
+            block = torch.zeros((internal.shape[0], S), dtype=torch.bool)
+            block = self.get_external_indices(block, e, size_internal)
+            block[:, pathway] = internal
+            rows_of.append([int(order[e])] * block.shape[0])
+            sizes_of.append([len(pathway)] * block.shape[0])
+            blocks.append(block)
+            if cumulative > total and S > 4000:
+                break
+            cumulative += block.shape[0]
+        mask = torch.cat(blocks, dim=0)
+        prow = torch.tensor(list(itertools.chain.from_iterable(rows_of)), dtype=torch.int)
+        psize = torch.tensor(list(itertools.chain.from_iterable(sizes_of)), dtype=torch.int)
+        if S > 4000 and mask.shape[0] > total:
             ind = torch.argsort(psize, descending=True)[:total]
         else:
             ind = torch.randperm(mask.shape[0])
-        mask = mask[ind]
-        if prow is not None:
-            prow = prow[ind]
-        return mask, prow
+        return mask[ind], prow[ind]
 
     def generate_bits(self, device):
         """Compat sampler straight to bit-packed device rows: (bits int32 [R, W], pathway_rows).
-        Community masks: `generate` then packed on the device.  Shapley masks (no communities):
+        Community masks: the native replay of the reference's draws (`_community_bits`), then
+        uploaded.  Shapley masks (no communities):
         the same torch CPU draws replayed natively as packed rows (engine.compat_shapley_bits),
         then the reference's randperm row shuffle applied on the device -- bit-identical rows
         and the same generator state afterwards, without the [R, S] bool tensor and its host
         row gather (masks.py:231-260, 375-380)."""
         from . import engine
         if self.pathways is not None:
-            mask, prow = self.generate()
-            if torch.device(device).type == "cpu":  # host callers: the same packing with torch ops
-                R, S = mask.shape
-                W = (S + 31) // 32
-                m = torch.zeros((R, W * 32), dtype=torch.int64)
-                m[:, :S] = mask
-                w = (m.view(R, W, 32) << torch.arange(32, dtype=torch.int64)).sum(-1)
-                return w.to(torch.uint32).view(torch.int32) if hasattr(torch, "uint32") else \
-                    ((w + 2 ** 31) % 2 ** 32 - 2 ** 31).to(torch.int32), prow
-            return engine.pack_masks(mask.to(device)), (prow.to(device) if prow is not None else None)
+            bits, prow = self._community_bits()
+            dev = torch.device(device)
+            if dev.type == "cpu":
+                return bits, prow
+            return bits.to(dev, non_blocking=True), prow.to(dev, non_blocking=True)
         n_perturbs, epochs = self.assertions_mask_generator(self.params)
         size = torch.Size((n_perturbs * epochs, self.element_count()))  # torch.randint's checks
         host = engine.compat_shapley_bits(size[0], size[1])
@@ -202,3 +243,9 @@ class Mask(Data):
         if prow is not None:
             prow = prow.to(device)
         return self.mask_loader(mask, epochs), prow
+
+
+def _unpack_host(bits, cols):
+    """Bit-packed int32 [R, W] host rows -> bool [R, cols] (bit c % 32 of word c // 32)."""
+    b = bits.contiguous().numpy().view(np.uint8).reshape(bits.shape[0], -1)
+    return torch.from_numpy(np.unpackbits(b, axis=1, bitorder="little")[:, :cols].copy()).bool()

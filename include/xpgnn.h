@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 15
+#define XPG_ABI_VERSION 16
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -84,6 +84,20 @@ int xpg_sample_shapley_dev(const uint64_t* seed, int64_t row_offset, int64_t row
  * torch.set_rng_state).  Bit-identical to the torch draw (v15). */
 int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t rows, int64_t cols,
                           uint32_t* bits);
+/* HOST function (no GPU work): the reference's compat COMMUNITY draws (Mask.mask_generator with
+ * communities, masks.py:299-348: per community in length-descending order get_internal_mask's
+ * randint masks.py:130, Pathways.mask_generator's antithetic randint rows pathways.py:260-281,
+ * activate_dead_mask's randperm pathways.py:318, pathway_mask2node_mask pathways.py:336-385 and
+ * the member assignment masks.py:338) replayed from the at::mt19937 state as above, written
+ * UNSHUFFLED as bit-packed rows bits[rows][ceil(cols/32)] (host memory); the caller applies the
+ * row shuffle (torch.randperm, masks.py:385, on the returned state) or the S > 4000 truncation.
+ * comm_ptr / comm_cols: CSR [n_comm + 1] / [nnz] of every community's member columns, ascending
+ * (the reference sorts each community in place, masks.py:323); blocks: int32 [n_blocks][5] =
+ * {row_start, size, size_internal, own community, b} back to back (Mask.community_plan), rows =
+ * their total.  Bit-identical to the torch path, state advanced exactly as torch would (v16). */
+int xpg_mt19937_community_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t cols,
+                               int32_t n_comm, const int32_t* comm_ptr, const int32_t* comm_cols,
+                               const int32_t* blocks, int32_t n_blocks, int64_t rows, uint32_t* bits);
 /* Same bits, plus counts[r] = popcount of row r (the KernelSHAP coalition sizes, kernels.py:144),
  * accumulated while sampling so KernelSHAP needs no second pass over the bits. */
 int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,

@@ -654,11 +654,63 @@ def test_explainer_query_cache_same_results():
     assert df1.equals(df2)
     df3, _ = Explainer(feat, ei, arch, params, names).run("11", 1)
     assert df1.equals(df3)
+    assert exp.last_run["query_cache"] == "hit"
     with torch.no_grad():
         feat.mul_(1.0)
     exp.run("11", 1)
     assert exp.last_run["arch_check"] == "cached"  # the module check is still valid ...
-    assert len(exp._queries) == 2                   # ... but the query was prepared again
+    assert exp.last_run["query_cache"] == "miss"    # ... but the query was prepared again
+    assert len(exp._queries) == 1
+
+
+def test_explainer_query_cache_stale_inputs():
+    """The per-query cache never answers for changed inputs: a NEW same-shape
+    feature tensor swapped in after the old one was freed (the caching allocator hands the new
+    one the freed address, version 0), a middle name edited in place inside the subgraph, and
+    the element's name moved elsewhere all prepare the query again, and each result equals a
+    fresh Explainer's on the same inputs."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    g = torch.Generator().manual_seed(23)
+    n, f = 400, 8
+    feat_a = torch.randn((n, f), generator=g)
+    feat_b = torch.randn((n, f), generator=g)
+    ei = torch.randint(0, n, (2, 2000), generator=g).to(DEV)
+    torch.manual_seed(23)
+    arch = ConvStack("gcn", [f, 16, 16], [16, 1]).eval()
+    params = {"seed": 6, "interpret_samples": 32, "epochs": 8, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": "device"}
+    names = [str(i) for i in range(n)]
+    exp = Explainer(feat_a.to(DEV), ei, arch, params, names)
+    exp.run("13", 1)
+    ptr_a = exp.feat.data_ptr()
+    exp.feat = None
+    torch.cuda.synchronize()
+    exp.feat = feat_b.to(DEV)                    # often at ptr_a again, with _version 0
+    df, _ = exp.run("13", 1)
+    assert exp.last_run["query_cache"] == "miss", (ptr_a, exp.feat.data_ptr())
+    df_f, _ = Explainer(feat_b.to(DEV), ei, arch, params, list(names)).run("13", 1)
+    assert df.equals(df_f)
+    exp.run("13", 1)
+    assert exp.last_run["query_cache"] == "hit"
+    # a name inside the subgraph (not the element) renamed in place
+    sub = exp.last_run["plan"].frontiers[0]
+    other = int(next(nm for nm in sorted(df.index) if nm != "13"))
+    names[other] = "renamed"
+    df2, _ = exp.run("13", 1)
+    assert exp.last_run["query_cache"] == "miss"
+    assert "renamed" in set(df2.index)
+    df2_f, _ = Explainer(feat_b.to(DEV), ei, arch, params, list(names)).run("13", 1)
+    assert df2.equals(df2_f)
+    # the element's name moved: position 13 renamed, another position takes "13"
+    names[13], names[n - 1] = "x13", "13"
+    df3, _ = exp.run("13", 1)
+    assert exp.last_run["query_cache"] == "miss"
+    df3_f, _ = Explainer(feat_b.to(DEV), ei, arch, params, list(names)).run("13", 1)
+    assert df3.equals(df3_f)
+    assert len(sub) > 0
+    exp.clear_cache()
+    assert not exp._queries
 
 
 def test_explainer_arch_check_keyed_on_query_lowering():

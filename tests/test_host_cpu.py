@@ -96,6 +96,11 @@ def test_extract_index_follows_in_place_name_edits():
     with pytest.raises(AssertionError):
         Explainer.extract_index("n3", names)
     assert Explainer.extract_index(12, None) == 12
+    # membership is the names' own (explainer.py:222 `element in names`): '5' is no member of
+    # integer names, even though numpy's str form of 5 is '5' 
+    ints = list(range(10))
+    with pytest.raises(AssertionError):
+        Explainer.extract_index("5", ints)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -292,6 +297,115 @@ def test_community_plan_matches_compat_blocks(S, lens, samples):
         assert np.array_equal(counts[b[:, 3]], b[:, 1])
     else:  # truncation keeps the largest communities' rows first
         assert counts.sum() == out_rows and set(np.flatnonzero(counts)) <= set(b[:, 3].tolist())
+
+
+def _random_communities(S, lens, seed, overlap=False):
+    rng = np.random.default_rng(seed)
+    if overlap:  # members drawn independently: communities share columns
+        return [sorted(rng.choice(S, n, replace=False).tolist()) for n in lens]
+    perm = rng.permutation(S)
+    out, o = [], 0
+    for n in lens:
+        out.append(rng.permutation(perm[o:o + n]).tolist())  # unsorted: the sampler sorts
+        o += n
+    return out
+
+
+@pytest.mark.parametrize("S, lens, samples, overlap, pre", [
+    (1193, [60] * 19 + [53], 256, False, 0),          # the communities_c2 shape (c2 subgraph)
+    (300, [40, 7, 2, 1, 25, 60, 3], 100, False, 5),   # tiny communities: size_internal < 3
+    (64, [3, 2], 7, False, 623),                      # two communities: dead-mask randperm rows
+    (50, [1, 1, 1, 1], 3, True, 624),                 # single members, shared columns
+    (40, [40], 20, False, 1250),                      # one community (no external coalition)
+    (120, [30, 50, 10, 70], 33, True, 17),            # overlapping communities
+    (5000, [900, 700, 40, 30, 20, 10, 5], 30, False, 3),  # S > 4000: truncation branch
+])
+def test_native_community_draw_matches_torch(S, lens, samples, overlap, pre):
+    """The compat community sampler's native replay (Mask._community_bits ->
+    xpg_mt19937_community_bits, host code) equals the reference's torch call sequence
+    (Mask._generate_torch, itself pinned by the golden masks) bit for bit: same rows, same
+    pathway_rows, the caller's lists sorted the same way, and torch's generator left at the
+    same position, from several generator positions (fresh, mid-block, block boundaries)."""
+    from bikg_graph_explainability_public_amd.masks import _unpack_host
+    comms = _random_communities(S, lens, S + len(lens), overlap)
+    ref_lists, nat_lists = [list(c) for c in comms], [list(c) for c in comms]
+    torch.manual_seed(S * 3 + samples)
+    torch.randint(0, 2 ** 31, (pre,))
+    ref_mask, ref_prow = _plan_mask(S, ref_lists, samples)._generate_torch()
+    ref_after = torch.randint(0, 2 ** 31, (6,))
+    torch.manual_seed(S * 3 + samples)
+    torch.randint(0, 2 ** 31, (pre,))
+    bits, prow = _plan_mask(S, nat_lists, samples)._community_bits()
+    assert torch.equal(torch.randint(0, 2 ** 31, (6,)), ref_after)
+    assert torch.equal(_unpack_host(bits, S), ref_mask)
+    np.testing.assert_array_equal(bits.numpy().view(np.uint32), oracle.pack_bits(ref_mask.numpy()))
+    assert torch.equal(prow, ref_prow)
+    assert nat_lists == ref_lists
+
+
+def test_native_community_dead_mask_sweep(monkeypatch):
+    """Blocks whose external coalitions come out all-off take activate_dead_mask's randperm
+    (pathways.py:285-334; only when a block has at most one external row pair): 120 seeds of a
+    tiny 3-community problem, most of which take that branch at least once, replay bit-exactly
+    with the generator at the same position afterwards."""
+    from bikg_graph_explainability_public_amd.masks import _unpack_host
+    calls = []
+    orig = Pathways.activate_dead_mask
+    monkeypatch.setattr(Pathways, "activate_dead_mask",
+                        lambda self, *a: calls.append(1) or orig(self, *a))
+    comms = [[0, 1, 2], [3, 4], [5]]
+    for seed in range(120):
+        torch.manual_seed(seed)
+        m, p = _plan_mask(8, [list(c) for c in comms], 1)._generate_torch()
+        after = torch.randint(0, 2 ** 31, (3,))
+        torch.manual_seed(seed)
+        b, q = _plan_mask(8, [list(c) for c in comms], 1)._community_bits()
+        assert torch.equal(_unpack_host(b, 8), m) and torch.equal(p, q), seed
+        assert torch.equal(torch.randint(0, 2 ** 31, (3,)), after), seed
+    assert len(calls) > 50
+
+
+def test_native_community_generate_bits_golden_cases():
+    """Explainer-level compat draws through the native community replay reproduce the
+    reference's recorded masks of every golden case with communities (generate_bits)."""
+    hit = 0
+    for name in CASES:
+        exp, z, meta = build_explainer(name)
+        if exp.pathways is None:
+            continue
+        hit += 1
+        torch.set_rng_state(torch.as_tensor(z["rng_state"]))
+        if meta["times"] == 1:
+            set_seed(meta["params"]["seed"])
+        ctx = exp.prepare(meta["element"], torch.device("cpu"))
+        gold = repeat_masks(z, meta)
+        for i in range(meta["n_repeats"]):
+            m = Mask(ctx["sub_feat"], ctx["sub_ei"], ctx["sub_pw_inds"], exp.params, exp.problem)
+            bits, rows = m.generate_bits("cpu")
+            np.testing.assert_array_equal(bits.numpy().view(np.uint32), oracle.pack_bits(gold[i]))
+            if f"r{i}_pathway_rows" in z.files:
+                assert np.array_equal(rows.numpy(), z[f"r{i}_pathway_rows"])
+            w0 = LinearRegression(ctx["S"]).layer.weight.detach().numpy().reshape(-1)
+            assert np.array_equal(w0, z[f"r{i}_w0"])
+            dataloader_seed_draw()
+    assert hit >= 1
+
+
+def test_community_plan_sizes_equal_internal_sizes():
+    """community_plan computes every block's (size, size_internal) in one float32 tensor pass;
+    they equal the reference's per-community internal_sizes (masks.py:98-125, a float32 0-d
+    tensor fraction per call) over many random community length sets and totals."""
+    rng = np.random.default_rng(7)
+    for trial in range(200):
+        n = int(rng.integers(1, 40))
+        lens = rng.integers(1, 3000 if trial % 2 else 30, n).tolist()
+        samples = int(rng.integers(1, 600))
+        epochs = int(rng.integers(1, 60))
+        comms = [list(range(k)) for k in lens]
+        blocks, _, _, _ = _plan_mask(max(lens) + 1, comms, samples, epochs).community_plan()
+        lt = torch.tensor(lens)
+        for row in blocks.tolist():
+            assert (row[1], row[2]) == Mask.internal_sizes(lens[row[3]], lt, samples * epochs)
 
 
 def test_community_columns_csr():
