@@ -351,7 +351,7 @@ def headline(args, dev, world, rank, workload="c2"):
     params = {"lr": 0.01, "l1_lambda": 1e-4}
     stream = torch.cuda.current_stream()
     side = torch.cuda.Stream(device=dev)
-    use_side = os.environ.get("XPG_SIDE_STREAM") != "0"  # sharding.gather_map_beside's switch
+    use_side = True  # KernelSHAP beside the forward, as sharding.gather_map_beside runs it
     w0 = torch.zeros((times, S), device=dev)
     statuses = []
     phases = ("sample", "forward", "shap", "gather", "wlm")

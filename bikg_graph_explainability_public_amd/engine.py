@@ -12,7 +12,6 @@ All device memory is owned by torch tensors held by the plan; the C-ABI never al
 """
 import contextlib
 import ctypes
-import os
 import gc
 import itertools
 import math
@@ -433,6 +432,11 @@ def plan_arrays(S, rel_np, queries, L, rel_eid=None):
             "deg_eid": deg_eid, "layers": layers}
 
 
+# ForwardPlan drops the relation terms of other destination types from a layer whose targets
+# share one node type (they add exactly 0); False keeps every term (the parity suite's reference)
+PLAN_DROP_OTHER_TYPES = True
+
+
 class ForwardPlan:
     """Receptive-field plan of one (subgraph, model program, query set)."""
 
@@ -515,7 +519,7 @@ class ForwardPlan:
                 # destination), so it is dropped — fewer aggregate columns and a shorter K of
                 # the layer's dense product (the query layer of a multi-type plan)
                 tt = np.unique(nt_np[fr[lvl]])
-                if tt.size == 1 and os.environ.get("XPG_PLAN_ALL_TERMS") != "1":  # (A/B switch)
+                if tt.size == 1 and PLAN_DROP_OTHER_TYPES:
                     kept = [t for t in terms if t.dst_type < 0 or t.dst_type == int(tt[0])]
                     terms = kept or terms
             self.terms_kept.append(len(terms))

@@ -9,7 +9,6 @@ Architectures the engine cannot compile run through `generic_outputs` (the user'
 on the B-fold union graph built with the HIP edge-keep kernel) — still on the GPU, with the
 KernelSHAP and surrogate stages unchanged.
 """
-import os
 import warnings
 
 import torch
@@ -19,6 +18,10 @@ from .data import Data
 from .model import Model
 from .program import UnsupportedArch, compile_arch
 
+
+# generic multi-node-type path: one arch call over the per-type disjoint union of the copies
+# (False: the reference's per-copy loop, model.py:118-253)
+HETERO_BATCHED = True
 
 def relation_edges(edge_index, edge_type, n_rel):
     if edge_type is None:
@@ -195,10 +198,10 @@ def generic_outputs(arch, feat, edge_index, mask, element_index, problem, node_t
         if n_types < 2:
             out = mc.infer(cf, pei, cnt, pet)
         else:
-            # one arch call over the disjoint union per node type (§8f2); XPG_HETERO_LOOP=1
-            # restores the reference's per-copy loop
+            # one arch call over the disjoint union per node type (§8f2); HETERO_BATCHED =
+            # False restores the reference's per-copy loop
             out = None
-            if os.environ.get("XPG_HETERO_LOOP", "0") != "1":
+            if HETERO_BATCHED:
                 out = mc.predict_hetero_output_batched(cf, pei, cnt, pet, node_type_names,
                                                        edge_type_names, B, S, element_index,
                                                        padded_dims, problem)

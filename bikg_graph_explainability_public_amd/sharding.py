@@ -14,7 +14,6 @@ Every rank ends with the same full tensors, so `weight_stacking` (mean / populat
 repeats) and the DataFrames are identical on every rank and identical to a single-GPU run.
 torch.distributed's all_gather needs equal shard shapes: shards are padded to the largest one.
 """
-import os
 
 import torch
 
@@ -177,7 +176,7 @@ def gather_map_beside(n, fn, side_fn, group=None):
     tensors / no GPU: sequential."""
     world, rank = world_info(group)
     s, e = shard_range(n, world, rank)
-    if not torch.cuda.is_available() or os.environ.get("XPG_SIDE_STREAM") == "0":
+    if not torch.cuda.is_available():
         return gather_rows(fn(s, e), n, group), gather_rows(side_fn(s, e), n, group)
     cur = torch.cuda.current_stream()
     side = _side_stream(cur.device)

@@ -29,39 +29,22 @@ def _eng():
     return engine
 
 
-@pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-mfma", "wide-gather", "wide-exact",
-                        "wide-teams", "wide-nopipe", "wide-noct", "wide-rp4", "wide-noth",
-                        "wide-nosort", "wide-late"])
+@pytest.fixture(params=["rows", "fused", "unfused", "wide", "wide-exact", "wide-gather"])
 def fwd_path(request, monkeypatch):
     """xpg_masked_forward has four HIP paths: the lanes-=-rows fused kernel for 1-2 layer plans
     (default for small frontiers), the wave-per-row fused kernel (XPG_FORWARD=fused), the
     32-samples-per-pass wide path for 2-layer plans (XPG_FORWARD=wide; default for frontiers of
     8192+ nodes) and the multi-kernel path (XPG_FORWARD=unfused, also the fallback for plans the
-    others do not take; "wide-mfma" / "wide-gather" = the wide path with its MFMA / 16-lane-group
-    gather layer-1 kernel instead of the default one-wave-per-target k_wide_l1s; "wide-exact" =
-    layer 2 on the exact fp32 MFMA instead of the three-piece bf16 products; "wide-teams" = the
-    layer-2 kernel with two gather teams, two targets in flight per interval; "wide-nopipe" = the
-    B3 layer-2 kernel without the cross-target pipelined gather; "wide-noct" = h1 holds every
-    sample's row (no inactive-row table); "wide-rp4" = 4 prefetched kept rows per group (default 6))."""
+    others do not take).  "wide-exact" = layer 2 on the exact fp32 MFMA instead of the
+    three-piece bf16 products (XPG_WIDE_B3=0); "wide-gather" = the wide path with its
+    16-lane-group gather layer-1 kernel instead of k_wide_l1s (the kernel plans that k_wide_l1s
+    does not take run; a diagnostics switch)."""
     monkeypatch.setenv("XPG_FORWARD", request.param.split("-")[0])
-    if request.param in ("wide-mfma", "wide-gather"):
-        monkeypatch.setenv("XPG_WIDE_L1", request.param.split("-")[1])
     if request.param == "wide-exact":
         monkeypatch.setenv("XPG_WIDE_B3", "0")
-    if request.param == "wide-teams":
-        monkeypatch.setenv("XPG_WIDE_TEAMS", "2")
-    if request.param == "wide-nopipe":
-        monkeypatch.setenv("XPG_WIDE_PIPE", "0")
-    if request.param == "wide-noct":
-        monkeypatch.setenv("XPG_WIDE_CT", "0")
-    if request.param == "wide-rp4":
-        monkeypatch.setenv("XPG_WIDE_RP", "4")
-    if request.param == "wide-noth":  # layer 2 without the transposed product (32-lane head reduction)
-        monkeypatch.setenv("XPG_WIDE_TH", "0")
-    if request.param == "wide-nosort":  # gather group g takes sample g (no active-first order)
-        monkeypatch.setenv("XPG_WIDE_SORT", "0")
-    if request.param == "wide-late":  # the next target's rows issued after the A tile is stored
-        monkeypatch.setenv("XPG_WIDE_EARLY", "0")
+    if request.param == "wide-gather":
+        monkeypatch.setenv("XPG_DIAGNOSTICS", "1")
+        monkeypatch.setenv("XPG_WIDE_L1_GATHER", "1")
     return request.param
 
 
@@ -262,7 +245,7 @@ def test_community_sampler_structure(S, lens, samples):
 def test_community_sampler_column_masks_equal_per_column_rule(S, lens, samples, overlap,
                                                               monkeypatch):
     """The column-bitmask sampler (one mask per community in LDS, a word per lane) writes the
-    same bits and pathway rows as the per-column lookup (XPG_COMM_CM=0), overlapping members
+    same bits and pathway rows as the per-column lookup (XPG_COMM_PERCOL=1), overlapping members
     included, shuffled / unshuffled, whole repeat and row ranges (words > 64 too)."""
     e = _eng()
     pathways, _ = _community_case(S, lens, samples)
@@ -275,8 +258,9 @@ def test_community_sampler_column_masks_equal_per_column_rule(S, lens, samples, 
                 {"interpret_samples": samples, "epochs": 2}, "node_prediction").community_plan()
     blocks, src_rows, rows, _ = plan
     outs = {}
+    monkeypatch.setenv("XPG_DIAGNOSTICS", "1")
     for mode in ("0", "1"):
-        monkeypatch.setenv("XPG_COMM_CM", mode)
+        monkeypatch.setenv("XPG_COMM_PERCOL", "1" if mode == "0" else "0")
         outs[mode] = [e.sample_communities(s, (blocks, src_rows, src_rows, sh), pathways, S, DEV)
                       for s in (5, 9) for sh in (False, True)]
         outs[mode].append(e.sample_communities(5, plan, pathways, S, DEV, row_offset=rows // 3,
@@ -1048,11 +1032,11 @@ def test_multi_type_engine_vs_oracle_random(hidden, layers):
 @pytest.mark.parametrize("hidden", [32, 64])
 def test_layer1_rows_kernel_and_term_dropping_bitwise(hidden, monkeypatch):
     """The multi-kernel path's layer-1 aggregation with lanes = mask rows (k_agg_l1_rows, the
-    default at widths 32 / 64) against the generic k_agg<true> (XPG_AGG_ROWS=0), bitwise, on a
+    default at widths 32 / 64) against the generic k_agg<true> (XPG_AGG_GENERIC=1), bitwise, on a
     multi-type MEAN + ROOT plan (whose reduced in-degree table makes MEAN sources test their own
     mask bit) and on a homogeneous GCN plan; and the ForwardPlan lowering that drops the other
     destination types' relation terms from a single-type layer (the query layer here) against
-    the all-terms plan (XPG_PLAN_ALL_TERMS=1): fewer terms, the same outputs."""
+    the all-terms plan (engine.PLAN_DROP_OTHER_TYPES = False): fewer terms, the same outputs."""
     from bikg_graph_explainability_public_amd import pipeline
     from bikg_graph_explainability_public_amd.nn import ConvStack, HeteroSageStack
     from golden_utils import multi_type_setup
@@ -1078,15 +1062,16 @@ def test_layer1_rows_kernel_and_term_dropping_bitwise(hidden, monkeypatch):
     m[0], m[1] = False, True
     bits = e.pack_masks(torch.as_tensor(m, device=DEV))
     plan, _ = _mt_plan(c, arch.to(DEV))
-    monkeypatch.delenv("XPG_AGG_ROWS", raising=False)
+    monkeypatch.setenv("XPG_DIAGNOSTICS", "1")
+    monkeypatch.delenv("XPG_AGG_GENERIC", raising=False)
     y_rows = plan.forward(bits)
-    monkeypatch.setenv("XPG_AGG_ROWS", "0")
+    monkeypatch.setenv("XPG_AGG_GENERIC", "1")
     y_gen = plan.forward(bits)
-    monkeypatch.delenv("XPG_AGG_ROWS")
+    monkeypatch.delenv("XPG_AGG_GENERIC")
     assert torch.equal(y_rows, y_gen)
-    monkeypatch.setenv("XPG_PLAN_ALL_TERMS", "1")
+    monkeypatch.setattr(e, "PLAN_DROP_OTHER_TYPES", False)
     plan_all, _ = _mt_plan(c, arch)
-    monkeypatch.delenv("XPG_PLAN_ALL_TERMS")
+    monkeypatch.setattr(e, "PLAN_DROP_OTHER_TYPES", True)
     assert plan.terms_kept[-1] < plan_all.terms_kept[-1]
     np.testing.assert_allclose(plan_all.forward(bits).cpu().numpy(), y_rows.cpu().numpy(),
                                rtol=0, atol=1e-6)
@@ -1099,9 +1084,9 @@ def test_layer1_rows_kernel_and_term_dropping_bitwise(hidden, monkeypatch):
     hp = pipeline.build_plan(gcn, x.to(DEV), eih.to(DEV), [9])
     mh = gm.random((130, hp.cols)) < 0.6
     bh = e.pack_masks(torch.as_tensor(mh, device=DEV))
-    monkeypatch.delenv("XPG_AGG_ROWS", raising=False)
+    monkeypatch.delenv("XPG_AGG_GENERIC", raising=False)
     yh_rows = hp.forward(bh)
-    monkeypatch.setenv("XPG_AGG_ROWS", "0")
+    monkeypatch.setenv("XPG_AGG_GENERIC", "1")
     yh_gen = hp.forward(bh)
     assert torch.equal(yh_rows, yh_gen)
 

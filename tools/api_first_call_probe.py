@@ -7,6 +7,7 @@ phase clock gives host / device ms per phase.
 """
 import argparse
 import collections
+import gc
 import os
 import sys
 import time
@@ -36,6 +37,14 @@ def main():
     p.add_argument("--queries", default="8,9,10,11,12,13,10,14")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
+    gc_t = {}
+
+    def gc_cb(phase, info):  # Python's cyclic collections, timed
+        if phase == "start":
+            gc_t["t"] = time.perf_counter()
+        else:
+            LOG.append((f"gc gen{info['generation']}", (time.perf_counter() - gc_t["t"]) * 1e3))
+    gc.callbacks.append(gc_cb)
     orig_call = _lib.call
 
     def call(name, *a):
@@ -55,6 +64,8 @@ def main():
     params = {"seed": 1, "interpret_samples": 256, "epochs": 50, "optimizer": "adam", "lr": 0.01,
               "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": "device"}
     exp = Explainer(feat.to(dev), ei.to(dev), arch, params, [str(i) for i in range(n)])
+    if os.environ.get("PROBE_GC_FREEZE") == "1":  # the inputs (100k names ...) out of the collector's way
+        gc.freeze()
     for q in args.queries.split(","):
         LOG.clear()
         torch.cuda.synchronize()

@@ -25,6 +25,9 @@ for step in "$@"; do
     # both ranks on cuda:0 (the driver's 8-GPU runs use RCCL, one GPU per rank)
     rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
     capture) run capture 400 python tools/capture_probe.py ;;
+    apitrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+              run apitrace 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d gpurun_out/apitrace -o run -- python3 tools/api_first_call_probe.py --queries 8,9,10 ;;
+    overlap) run overlap 500 python tools/ws_ab.py --rows 256 --reps 3 --variants "OVERLAP=0;OVERLAP=1;OVERLAP=0;OVERLAP=1" ;;
     rank2c4) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2c4 500 python bench.py --gpus 2 --sections c4 --no-cpu-baseline && run rank1c4 300 python bench.py --sections c4 --no-cpu-baseline && grep -h result_checksum gpurun_out/rank2c4.log gpurun_out/rank1c4.log | python -c "import sys, json; [print(json.loads(l)['n_gpus'], json.loads(l)['regimes']['hetero_c4']['result_checksum'], json.loads(l)['regimes']['hetero_c4']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     rank2c5) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2c5 500 python bench.py --gpus 2 --sections c5 --no-cpu-baseline && run rank1c5 300 python bench.py --sections c5 --no-cpu-baseline && grep -h result_checksum gpurun_out/rank2c5.log gpurun_out/rank1c5.log | python -c "import sys, json; [print(json.loads(l)['n_gpus'], json.loads(l)['regimes']['c5_hetero']['result_checksum'], json.loads(l)['regimes']['c5_hetero']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     c5info) run c5info 300 python -u tools/c5_plan_info.py ;;
@@ -55,7 +58,7 @@ for step in "$@"; do
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
     widetests) run widetests 600 python -u -m pytest tests/test_gpu_coverage.py tests/test_gpu_parity.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wide or c3 or hub" ;;
     idxab) run idxab 600 python -u tools/ws_ab.py --variants "${IDXAB:-B3=1,IDX=0;B3=1;B3=1,IDX=0;B3=1;B3=1,RP=6}" ;;
-    probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 && XPG_MC_XCD=0 run probe_mc_noxcd 120 ./tools/wlm_probe 1193 12800 256 ;;
+    probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 ;;
     profall) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run profall 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profall -o run -- python3 bench.py --no-cpu-baseline ;;
     benchall) run benchall 900 python bench.py ;;

@@ -2,7 +2,7 @@
 full-graph forward (1M nodes / 10M edges, 2-layer SAGE 128, every node a target), one plan,
 one 32-row pass per variant; outputs compared with the exact f32 variant (XPG_WIDE_B3=0).
 
-    python tools/ws_ab.py [--nodes N] [--edges E] [--variants "B3=0;B3=1;B3=1,TEAMS=2"]
+    python tools/ws_ab.py [--nodes N] [--edges E] [--variants "B3=0;B3=1;OVERLAP=0"]
 """
 import argparse
 import os
@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bikg_graph_explainability_public_amd import _lib, engine, pipeline  # noqa: E402
 from bikg_graph_explainability_public_amd.nn import ConvStack  # noqa: E402
 
-KEYS = ("B3", "TEAMS", "GW", "L1", "WS", "WSKW", "DBG", "PIPE", "RP", "CT", "IDX", "TH", "SORT", "EARLY")
+KEYS = ("B3", "L1_GATHER", "DBG", "OVERLAP")
 
 
 def set_env(spec):
@@ -24,7 +24,7 @@ def set_env(spec):
     for kv in filter(None, spec.split(",")):
         k, v = kv.split("=")
         os.environ["XPG_WIDE_" + k] = v
-    if "DBG=" in spec:  # ablation switches need the diagnostics opt-in
+    if "DBG=" in spec or "L1_GATHER=" in spec:  # diagnostics switches need the opt-in
         os.environ["XPG_DIAGNOSTICS"] = "1"
     else:
         os.environ.pop("XPG_DIAGNOSTICS", None)
@@ -37,7 +37,7 @@ def main():
     p.add_argument("--feat", type=int, default=128)
     p.add_argument("--rows", type=int, default=32)
     p.add_argument("--reps", type=int, default=3)
-    p.add_argument("--variants", default="B3=0;B3=1;B3=1,TEAMS=2;B3=0,TEAMS=2")
+    p.add_argument("--variants", default="B3=0;B3=1;B3=1,L1_GATHER=1")
     args = p.parse_args()
     dev = torch.device("cuda", 0)
     _lib.load()
