@@ -138,8 +138,9 @@ class Explainer:
                 "No element names have been given and the node name given is not numeric"
             return int(element)
         if isinstance(element, str):
-            members, idx = _name_index(names, element)
-            assert element in members, "Element name '{}' is not present in the graph".format(element)
+            idx = _name_index(names, element)
+            assert _is_member(element, names, idx), \
+                "Element name '{}' is not present in the graph".format(element)
             return idx[element]
         assert element in names, "Element name '{}' is not present in the graph".format(element)
         return int(np.where(np.array(names, dtype=str) == element)[0][0])
@@ -635,37 +636,43 @@ _NAME_INDEX = {}
 
 
 def _name_index(names, element=None):
-    """(members, {str(name): first position}) of a names list — the reference's
-    `element in names` (members = set(names) of the names themselves, not their str forms: a
-    '5' is not a member of [5], as explainer.py:222 asserts) and its
-    np.where(np.array(names, dtype=str) == element)[0][0] as lookups — cached by identity and
+    """{str(name): first position} of a names list — the reference's
+    np.where(np.array(names, dtype=str) == element)[0][0] as a lookup — cached by identity and
     length.  A hit is validated against the list itself (the cached position of `element` must
-    still hold it, and a name missing from the cached set is looked for again), so a list edited
-    in place is re-indexed instead of answering from a stale index; an edit that adds an EARLIER
-    copy of an indexed name at the same length is not detected."""
+    still hold it, and a name missing from the index is looked for again), so a list edited in
+    place is re-indexed instead of answering from a stale index; an edit that adds an EARLIER
+    copy of an indexed name at the same length is not detected.  The index is a dict of str ->
+    int (not tracked by Python's cyclic collector): a set or list of 1M names built per query
+    would be traversed by the next collections (~3 ms each for 100k names, the first-call
+    pauses of round 4)."""
     key = (id(names), len(names))
     hit = _NAME_INDEX.get(key)
     if hit is not None and hit[0] is names:
-        members, idx = hit[1], hit[2]
+        idx = hit[1]
         if element is None:
-            return members, idx
+            return idx
         i = idx.get(element)
         if i is not None and str(names[i]) == element:
-            return members, idx
+            return idx
         if i is None and element not in names:
-            return members, idx  # truly absent: the caller's assertion reports it
-    strs = np.array(names, dtype=str).tolist() if len(names) else []
+            return idx  # truly absent: the caller's assertion reports it
     idx = {}
-    for i, n in enumerate(strs):
+    for i, n in enumerate(np.array(names, dtype=str).tolist() if len(names) else []):
         idx.setdefault(n, i)
-    try:
-        members = set(names)
-    except TypeError:  # unhashable names: `element in names` on the list itself
-        members = names
     if len(_NAME_INDEX) > 8:
         _NAME_INDEX.clear()
-    _NAME_INDEX[key] = (names, members, idx)
-    return members, idx
+    _NAME_INDEX[key] = (names, idx)
+    return idx
+
+
+def _is_member(element, names, idx):
+    """The reference's `element in names` (explainer.py:222) for a str element: membership of
+    the names themselves, not of their str forms ('5' is no member of [5]); O(1) when the name
+    at the element's indexed position is the element itself (str names), else a scan."""
+    i = idx.get(element)
+    if i is None:
+        return False
+    return names[i] == element or element in names
 
 
 def _snapshot(x):

@@ -172,9 +172,14 @@ class GATConv(MessagePassing):
 
     def forward(self, x, edge_index):
         H, C = self.heads, self.out_channels
-        xs, xd = (x, x) if isinstance(x, torch.Tensor) else x
-        hs = self.lin_src(xs).view(-1, H, C)
-        hd = hs if (xd is xs and self.lin_dst is self.lin_src) else self.lin_dst(xd).view(-1, H, C)
+        # gat_conv.py (2.0.4): a Tensor input is transformed by lin_src for BOTH ends, also when a
+        # separate lin_dst exists (tuple in_channels: HeteroConv hands same-type relations a
+        # Tensor); a tuple input by lin_src / lin_dst
+        if isinstance(x, torch.Tensor):
+            hs = hd = self.lin_src(x).view(-1, H, C)
+        else:
+            hs = self.lin_src(x[0]).view(-1, H, C)
+            hd = self.lin_dst(x[1]).view(-1, H, C)
         a_s = (hs * self.att_src).sum(-1)
         a_d = (hd * self.att_dst).sum(-1)
         ei = edge_index.long()
@@ -281,6 +286,40 @@ class HeteroSageStack(nn.Module):
                                                         if li == 0 else (hidden, hidden), hidden)
                                      for r in rels}))
             convs.append(nn.ReLU())
+        self.conv = nn.ModuleList(convs)
+        fcs = []
+        for i in range(len(fc_dims) - 1):
+            fcs.append(Linear(fc_dims[i], fc_dims[i + 1]))
+            fcs.append(nn.Sigmoid() if i == len(fc_dims) - 2 else nn.ReLU())
+        self.fc = nn.ModuleList(fcs)
+
+    def forward(self, x, edge_index):
+        for i, c in enumerate(self.conv):
+            x = c(x, edge_index) if i % 2 == 0 else {k: c(v) for k, v in x.items()}
+        x = x[list(x.keys())[0]]
+        for layer in self.fc:
+            x = layer(x)
+        return x
+
+
+class HeteroGATStack(nn.Module):
+    """Multi-node-type model family of the reference's own multi-type test arch
+    (tests/test_utils.py:86-182: HeteroConv({(src, rel, dst): GATConv((-1, -1), c,
+    add_self_loops=False)}, aggr="sum") -> ReLU, then Linear layers on the first output node
+    type), with explicit input widths per layer and `heads` per layer (concatenated).  The
+    engine does not compile GAT: it runs on the generic (batched) torch path.  state_dict keys:
+    conv.<2l>.convs.<src>__<rel>__<dst>.{lin_src,lin_dst}.weight / att_src / att_dst / bias."""
+
+    def __init__(self, rels, in_dims, hidden, heads, fc_dims, add_self_loops=False):
+        super().__init__()
+        convs, width = [], None
+        for li, h in enumerate(heads):
+            convs.append(HeteroConv({tuple(r): GATConv((in_dims[r[0]], in_dims[r[-1]]) if li == 0
+                                                       else (width, width), hidden, heads=h,
+                                                       add_self_loops=add_self_loops)
+                                     for r in rels}))
+            convs.append(nn.ReLU())
+            width = hidden * h
         self.conv = nn.ModuleList(convs)
         fcs = []
         for i in range(len(fc_dims) - 1):

@@ -6,6 +6,7 @@ GCNConv (normalize=True, add_self_loops=True, improved=False, cached=False):
     out = scatter_add(norm_e * (x W^T)[row], col) + bias.     (lin before propagate, bias after)
 SAGEConv (aggr='mean', root_weight=True, normalize=False):
     out = lin_l(scatter_mean(x[row], col)) + lin_r(x)          (lin_r has no bias)
+GATConv: see the class docstring.
 HeteroConv(aggr='sum'): one conv per edge type keyed '__'.join(edge_type); outputs summed per
     destination node type in edge_index_dict order.
 Messages flow edge_index[0] (source) -> edge_index[1] (target).
@@ -84,11 +85,84 @@ class SAGEConv(MessagePassing):
 
 
 class GATConv(MessagePassing):
-    def __init__(self, *args, **kwargs):
-        super().__init__()
+    """GATConv (PyG 2.0.4 gat_conv.py) restated: lin_src (= lin_dst for an int in_channels;
+    separate lin_dst for a tuple, both bias-free, glorot), att_src / att_dst [1, H, C] (glorot),
+    bias [H*C] (concat) or [C] (zeros).  forward: a Tensor input is transformed by lin_src for
+    BOTH ends (even when a separate lin_dst exists); a tuple by lin_src / lin_dst.  alpha_src =
+    (x_src * att_src).sum(-1), alpha_dst likewise; add_self_loops: remove_self_loops then one
+    loop per node of min(|src|, |dst|); message alpha_j + alpha_i -> leaky_relu(0.2) -> softmax
+    over each target's in-edges (torch_geometric.utils.softmax: minus the per-target max, exp,
+    / (sum + 1e-16)) -> dropout (eval: none) -> x_j * alpha; sum per target; concat heads
+    (or mean) + bias.  Lazy in_channels (-1) materialise at the first forward."""
 
-    def forward(self, *args, **kwargs):  # pragma: no cover - not restated
-        raise NotImplementedError("GATConv is not restated by the PyG shim")
+    def __init__(self, in_channels, out_channels, heads=1, concat=True, negative_slope=0.2,
+                 dropout=0.0, add_self_loops=True, bias=True, **kwargs):
+        super().__init__()
+        self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
+        self.concat, self.negative_slope, self.dropout = concat, negative_slope, dropout
+        self.add_self_loops = add_self_loops
+        self.tuple_in = not isinstance(in_channels, int)
+        ins = in_channels if self.tuple_in else (in_channels, in_channels)
+        self._lazy = ins
+        self.lin_src = Linear(ins[0], heads * out_channels, bias=False, weight_initializer="glorot") \
+            if ins[0] > 0 else None
+        self.lin_dst = (Linear(ins[1], heads * out_channels, bias=False, weight_initializer="glorot")
+                        if ins[1] > 0 else None) if self.tuple_in else self.lin_src
+        self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
+        bound = (6.0 / (heads + out_channels)) ** 0.5
+        with torch.no_grad():
+            self.att_src.uniform_(-bound, bound)
+            self.att_dst.uniform_(-bound, bound)
+        self.bias = nn.Parameter(torch.zeros(heads * out_channels if concat else out_channels)) \
+            if bias else None
+
+    def _materialize(self, xs, xd):
+        if self.lin_src is None:
+            self.lin_src = Linear(xs.size(1), self.heads * self.out_channels, bias=False,
+                                  weight_initializer="glorot")
+            if not self.tuple_in:
+                self.lin_dst = self.lin_src
+        if self.tuple_in and self.lin_dst is None and xd is not None:
+            self.lin_dst = Linear(xd.size(1), self.heads * self.out_channels, bias=False,
+                                  weight_initializer="glorot")
+
+    def forward(self, x, edge_index):
+        H, C = self.heads, self.out_channels
+        if isinstance(x, torch.Tensor):
+            self._materialize(x, None)
+            x_src = x_dst = self.lin_src(x).view(-1, H, C)
+        else:
+            xs, xd = x
+            self._materialize(xs, xd)
+            x_src = self.lin_src(xs).view(-1, H, C)
+            x_dst = self.lin_dst(xd).view(-1, H, C) if xd is not None else None
+        a_src = (x_src * self.att_src).sum(-1)
+        a_dst = (x_dst * self.att_dst).sum(-1) if x_dst is not None else None
+        ei = edge_index.long()
+        n_dst = x_dst.size(0) if x_dst is not None else x_src.size(0)
+        if self.add_self_loops:
+            n = min(x_src.size(0), n_dst)
+            ei = ei[:, ei[0] != ei[1]]
+            loop = torch.arange(n, device=ei.device)
+            ei = torch.cat([ei, torch.stack([loop, loop])], 1)
+        src, dst = ei[0], ei[1]
+        alpha = a_src[src] if a_dst is None else a_src[src] + a_dst[dst]
+        alpha = torch.nn.functional.leaky_relu(alpha, self.negative_slope)
+        amax = torch.full((n_dst, H), float("-inf"), dtype=alpha.dtype)
+        amax = amax.scatter_reduce(0, dst.view(-1, 1).expand(-1, H), alpha, reduce="amax")
+        ex = (alpha - amax[dst]).exp()
+        den = torch.zeros((n_dst, H), dtype=alpha.dtype).index_add_(0, dst, ex)
+        alpha = ex / (den[dst] + 1e-16)
+        out = torch.zeros((n_dst, H, C), dtype=x_src.dtype).index_add_(0, dst,
+                                                                       x_src[src] * alpha.unsqueeze(-1))
+        out = out.reshape(n_dst, H * C) if self.concat else out.mean(dim=1)
+        if self.bias is not None:
+            out = out + self.bias
+        return out
+
+    def __repr__(self):
+        return f"GATConv({self.in_channels}, {self.out_channels}, heads={self.heads})"
 
 
 class HeteroConv(nn.Module):

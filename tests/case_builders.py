@@ -4,7 +4,7 @@ import copy
 import torch
 
 from bikg_graph_explainability_public_amd.explainer import Explainer
-from bikg_graph_explainability_public_amd.nn import ConvStack, HeteroSageStack
+from bikg_graph_explainability_public_amd.nn import ConvStack, HeteroSageStack, HeteroGATStack
 from golden_utils import case_inputs, load_case, state_dict
 
 
@@ -16,6 +16,11 @@ def _t(x):
 
 def build_arch(meta, z):
     a = meta["arch_spec"]
+    if a["kind"] == "hetero_gat":
+        arch = HeteroGATStack([tuple(r) for r in a["rels"]], a["in_dims"], a["hidden"],
+                              a["heads"], a["fc"])
+        arch.load_state_dict({k: torch.as_tensor(v) for k, v in state_dict(z).items()})
+        return arch.eval()
     if a["kind"] == "hetero_sage":
         arch = HeteroSageStack([tuple(r) for r in a["rels"]], a["in_dims"], a["hidden"],
                                a["layers"], a["fc"])

@@ -45,7 +45,7 @@ from pathway_explanations import explainer as pe_explainer  # noqa: E402
 from pathway_explanations import wlm as pe_wlm  # noqa: E402
 from pathway_explanations.masks import Mask as PeMask  # noqa: E402
 from pathway_explanations.kernels import Kernel as PeKernel  # noqa: E402
-from torch_geometric.nn import GCNConv, SAGEConv, HeteroConv, Linear  # noqa: E402
+from torch_geometric.nn import GATConv, GCNConv, SAGEConv, HeteroConv, Linear  # noqa: E402
 
 torch.set_num_threads(8)
 
@@ -107,6 +107,37 @@ class HeteroSage(nn.Module):
                                                  else (hidden, hidden), hidden) for r in rels},
                                     aggr="sum"))
             convs.append(nn.ReLU())
+        self.conv = nn.ModuleList(convs)
+        fcs = []
+        for i in range(len(fc_dims) - 1):
+            fcs.append(Linear(fc_dims[i], fc_dims[i + 1]))
+            fcs.append(nn.Sigmoid() if i == len(fc_dims) - 2 else nn.ReLU())
+        self.fc = nn.ModuleList(fcs)
+
+    def forward(self, x, edge_index):
+        for i, c in enumerate(self.conv):
+            x = c(x, edge_index) if i % 2 == 0 else {k: c(v) for k, v in x.items()}
+        x = x[list(x.keys())[0]]
+        for l in self.fc:
+            x = l(x)
+        return x
+
+
+class HeteroGat(nn.Module):
+    """The reference's multi-type test arch (tests/test_utils.py:86-182: HeteroConv of
+    GATConv(.., add_self_loops=False) per relation, sum, -> ReLU, then Linear layers on the first
+    output node type) with explicit input widths and `heads` per layer (concatenated)."""
+
+    def __init__(self, rels, in_dims, hidden, heads, fc_dims):
+        super().__init__()
+        convs, width = [], None
+        for li, h in enumerate(heads):
+            convs.append(HeteroConv({r: GATConv((in_dims[r[0]], in_dims[r[-1]]) if li == 0
+                                                else (width, width), hidden, heads=h,
+                                                add_self_loops=False) for r in rels},
+                                    aggr="sum"))
+            convs.append(nn.ReLU())
+            width = hidden * h
         self.conv = nn.ModuleList(convs)
         fcs = []
         for i in range(len(fc_dims) - 1):
@@ -308,6 +339,29 @@ def case_hetero_multi():
                         "fc": [16, 8, 1]})
 
 
+def case_hetero_gat():
+    """The multi-node-type path with the reference's own conv family (GATConv, tests/test_utils.py
+    :86-182): the hetero_multi graph (3 node types, 5 relations incl. the same-type 'aa', whose
+    conv gets a Tensor input), 2-layer HeteroConv(GAT) with 2 then 1 heads, add_self_loops=False.
+    GAT numerics come from the shim's PyG 2.0.4 restatement (parity pinned to it, as for GCN /
+    SAGE)."""
+    g = torch.Generator().manual_seed(41)
+    feat = {t: torch.randn((n, HM_DIMS[t]), generator=g) for t, n in HM_SIZES.items()}
+    ei = {r: torch.stack([torch.randint(0, HM_SIZES[r[0]], (m,), generator=g),
+                          torch.randint(0, HM_SIZES[r[-1]], (m,), generator=g)])
+          for r, m in zip(HM_RELS, (60, 50, 70, 30, 30))}
+    torch.manual_seed(13)
+    arch = HeteroGat(HM_RELS, HM_DIMS, 8, [2, 1], [8, 4, 1])
+    arch.eval()
+    names = {t: [f"{t.lower()}{i}" for i in range(n)] for t, n in HM_SIZES.items()}
+    torch.manual_seed(6)
+    run_case("hetero_gat", feat, ei, arch, dict(PARAMS, interpret_samples=16, epochs=4),
+             names, None, None, element_type="B", problem="node", element="b2", times=2,
+             arch_spec={"kind": "hetero_gat", "rels": [list(r) for r in HM_RELS],
+                        "sizes": HM_SIZES, "in_dims": HM_DIMS, "hidden": 8, "heads": [2, 1],
+                        "layers": 2, "fc": [8, 4, 1]})
+
+
 def case_sage_shapley():
     g = torch.Generator().manual_seed(5)
     n, e = 300, 1500
@@ -420,3 +474,4 @@ if __name__ == "__main__":
     case_gcn2_graph()
     case_gcn2_medium()
     case_hetero_multi()
+    case_hetero_gat()

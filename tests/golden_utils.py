@@ -84,10 +84,11 @@ def hetero_multi_setup(z, meta):
     feat, ei = case_inputs(z)
     a = meta["arch_spec"]
     return multi_type_setup(feat, ei, meta["names"], meta["element"], meta["element_type"],
-                            a["layers"], state_dict(z), a["fc"])
+                            a["layers"], state_dict(z), a["fc"], conv=a["kind"])
 
 
-def multi_type_setup(feat, ei, names_by_type, element, element_type, n_layers, sd, fc_dims):
+def multi_type_setup(feat, ei, names_by_type, element, element_type, n_layers, sd, fc_dims,
+                     conv="hetero_sage"):
     """hetero2homo (type blocks in feat-dict order, features zero-padded to the widest type,
     relation edges shifted by the node-type pointers, data.py:95-147,695-822), the L+1-hop
     computational subgraph of the element, and sub_ind = the element's position among the
@@ -113,6 +114,14 @@ def multi_type_setup(feat, ei, names_by_type, element, element_type, n_layers, s
     filt = [n for n, t in zip(sub_names, sub_nt) if t == etype]
     layers = []
     for li in range(n_layers):
+        if conv == "hetero_gat":  # GATConv((F_src, F_dst), c, heads, add_self_loops=False)
+            pre = lambda r: f"conv.{2 * li}.convs.{'__'.join(r)}."
+            layers.append({r: {"Ws": sd[pre(r) + "lin_src.weight"],
+                               "Wd": sd.get(pre(r) + "lin_dst.weight"),
+                               "att_s": sd[pre(r) + "att_src"], "att_d": sd[pre(r) + "att_dst"],
+                               "bias": sd.get(pre(r) + "bias"), "concat": True,
+                               "self_loops": False} for r in rels})
+            continue
         layers.append({r: {"Wl": sd[f"conv.{2 * li}.convs.{'__'.join(r)}.lin_l.weight"],
                            "bl": sd.get(f"conv.{2 * li}.convs.{'__'.join(r)}.lin_l.bias"),
                            "Wr": sd[f"conv.{2 * li}.convs.{'__'.join(r)}.lin_r.weight"]}

@@ -1091,15 +1091,22 @@ def test_layer1_rows_kernel_and_term_dropping_bitwise(hidden, monkeypatch):
     assert torch.equal(yh_rows, yh_gen)
 
 
-@pytest.mark.parametrize("path", ["engine", "generic"])
-def test_multi_type_explainer_run_matches_reference(path, monkeypatch):
-    """Explainer.run on the multi-node-type golden case (quirk Q4 reproduced) vs the
-    reference's DataFrames: the HIP engine and the batched generic path."""
+@pytest.mark.parametrize("case,path", [("hetero_multi", "engine"), ("hetero_multi", "generic"),
+                                       ("hetero_gat", "generic"), ("hetero_gat", "loop")])
+def test_multi_type_explainer_run_matches_reference(case, path, monkeypatch):
+    """Explainer.run on the multi-node-type golden cases (quirk Q4 reproduced) vs the
+    reference's DataFrames: the HIP engine and the batched generic path (HeteroConv of SAGE);
+    the reference's own multi-type conv, GATConv (the engine does not compile it: it runs on
+    the batched generic path, and on the reference's per-copy loop for comparison)."""
+    import warnings
     from bikg_graph_explainability_public_amd import pipeline
     from case_builders import build_explainer
-    if path == "generic":
+    if path == "generic" and case == "hetero_multi":
         monkeypatch.setattr(pipeline, "build_plan", lambda *a, **k: None)
-    exp, z, meta = build_explainer("hetero_multi")
+    if path == "loop":
+        monkeypatch.setattr(pipeline, "HETERO_BATCHED", False)
+    exp, z, meta = build_explainer(case)
+    warnings.simplefilter("ignore")
     torch.set_rng_state(torch.as_tensor(z["rng_state"]))
     df, _ = exp.run(meta["element"], meta["times"])
     assert exp.last_run["engine"] == (path == "engine")

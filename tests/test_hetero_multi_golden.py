@@ -1,15 +1,20 @@
 """Pin the oracle's multi-node-type restatement (oracle.hetero_multi_copy_outputs +
-hetero_multi_targets) against the reference run recorded in tests/golden/hetero_multi.*
-(make_golden.py case_hetero_multi: 3 node types, 5 relations, 2-layer HeteroConv(SAGE)).
-CPU only."""
+hetero_multi_targets) against the reference runs recorded in tests/golden/hetero_multi.* and
+hetero_gat.* (make_golden.py case_hetero_multi / case_hetero_gat: 3 node types, 5 relations,
+2-layer HeteroConv of SAGEConv / of GATConv — the reference's own multi-type test conv,
+tests/test_utils.py:86-182); and the package's GATConv (the generic path's torch layer) against
+the oracle's gat_conv.  CPU only."""
 import numpy as np
+import pytest
+import torch
 
 import oracle
 from golden_utils import hetero_multi_setup, load_case, repeat_masks
 
 
-def test_oracle_multi_type_targets_match_reference():
-    z, meta = load_case("hetero_multi")
+@pytest.mark.parametrize("name", ["hetero_multi", "hetero_gat"])
+def test_oracle_multi_type_targets_match_reference(name):
+    z, meta = load_case(name)
     c = hetero_multi_setup(z, meta)
     masks = repeat_masks(z, meta)
     S = c["x"].shape[0]
@@ -22,10 +27,11 @@ def test_oracle_multi_type_targets_match_reference():
         np.testing.assert_allclose(got, z[f"r{i}_output"], rtol=0, atol=2e-6)
 
 
-def test_oracle_multi_type_full_fit_matches_reference():
+@pytest.mark.parametrize("name", ["hetero_multi", "hetero_gat"])
+def test_oracle_multi_type_full_fit_matches_reference(name):
     """Targets -> KernelSHAP -> surrogate fit (Q1 with a single broadcast target) against the
     recorded final weights and losses."""
-    z, meta = load_case("hetero_multi")
+    z, meta = load_case(name)
     c = hetero_multi_setup(z, meta)
     masks = repeat_masks(z, meta)
     S = c["x"].shape[0]
@@ -42,3 +48,47 @@ def test_oracle_multi_type_full_fit_matches_reference():
         np.testing.assert_allclose(w, z[f"r{i}_w_final"], rtol=0, atol=2e-5)
         np.testing.assert_allclose(losses, z[f"r{i}_losses"], rtol=1e-4, atol=1e-9)
         assert best == meta[f"r{i}_best_epoch"]
+
+
+@pytest.mark.parametrize("heads,concat,loops,tuple_in", [(1, True, False, True), (2, True, False, True),
+                                                        (3, False, True, True), (2, True, True, False)])
+def test_package_gatconv_matches_oracle(heads, concat, loops, tuple_in):
+    """nn.GATConv (PyG 2.0.4 semantics) against oracle.gat_conv on random bipartite and
+    same-type graphs: multi-head concat / mean, with and without self-loops, duplicate edges and
+    targets without in-edges; a Tensor input uses lin_src for both ends (gat_conv.py 2.0.4)."""
+    from bikg_graph_explainability_public_amd.nn import GATConv
+    g = torch.Generator().manual_seed(heads * 10 + int(concat))
+    ns, nd, fs, fd, c = 23, 17, 6, 4, 5
+    torch.manual_seed(heads)
+    conv = GATConv((fs, fd) if tuple_in else fs, c, heads=heads, concat=concat,
+                   add_self_loops=loops).eval()
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    xs = torch.randn((ns, fs), generator=g, dtype=torch.float64)
+    xd = torch.randn((nd, fd), generator=g, dtype=torch.float64)
+    ei = torch.stack([torch.randint(0, ns, (70,), generator=g), torch.randint(0, nd - 3, (70,), generator=g)])
+    ei = torch.cat([ei, ei[:, :5]], 1)  # duplicate edges
+    conv = conv.double()
+    p = {"Ws": conv.lin_src.weight.detach().numpy(),
+         "Wd": conv.lin_dst.weight.detach().numpy(),
+         "att_s": conv.att_src.detach().numpy(), "att_d": conv.att_dst.detach().numpy(),
+         "bias": conv.bias.detach().numpy(), "concat": concat, "self_loops": loops}
+    with torch.no_grad():
+        got = conv((xs, xd), ei).numpy() if tuple_in else conv(xs, ei.clamp(max=ns - 1)).numpy()
+    if tuple_in:
+        ref = oracle.gat_conv(xs.numpy(), xd.numpy(), ei[0].numpy(), ei[1].numpy(), p, False)
+    else:
+        e2 = ei.clamp(max=ns - 1)
+        ref = oracle.gat_conv(xs.numpy(), xs.numpy(), e2[0].numpy(), e2[1].numpy(), p, True)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12)
+    if tuple_in:  # a same-type call of a tuple-initialised conv: W_src on both ends
+        x = torch.randn((ns, fs), generator=g, dtype=torch.float64)
+        conv2 = GATConv((fs, fs), c, heads=heads, concat=concat, add_self_loops=loops).double().eval()
+        e2 = ei.clamp(max=ns - 1)
+        p2 = dict(p, Ws=conv2.lin_src.weight.detach().numpy(), Wd=conv2.lin_dst.weight.detach().numpy(),
+                  att_s=conv2.att_src.detach().numpy(), att_d=conv2.att_dst.detach().numpy(),
+                  bias=conv2.bias.detach().numpy())
+        with torch.no_grad():
+            got2 = conv2(x, e2).numpy()
+        ref2 = oracle.gat_conv(x.numpy(), x.numpy(), e2[0].numpy(), e2[1].numpy(), p2, True)
+        np.testing.assert_allclose(got2, ref2, rtol=0, atol=1e-12)

@@ -27,6 +27,9 @@ for step in "$@"; do
     capture) run capture 400 python tools/capture_probe.py ;;
     apitrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
               run apitrace 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d gpurun_out/apitrace -o run -- python3 tools/api_first_call_probe.py --queries 8,9,10 ;;
+    htrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+            run htrace 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/htrace -o run -- python3 bench.py --sections headline --no-cpu-baseline --steps 20 ;;
+    apigc) run apigc 200 python -u tools/api_first_call_probe.py && PROBE_GC_FREEZE=1 run apigc_freeze 200 python -u tools/api_first_call_probe.py ;;
     overlap) run overlap 500 python tools/ws_ab.py --rows 256 --reps 3 --variants "OVERLAP=0;OVERLAP=1;OVERLAP=0;OVERLAP=1" ;;
     rank2c4) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2c4 500 python bench.py --gpus 2 --sections c4 --no-cpu-baseline && run rank1c4 300 python bench.py --sections c4 --no-cpu-baseline && grep -h result_checksum gpurun_out/rank2c4.log gpurun_out/rank1c4.log | python -c "import sys, json; [print(json.loads(l)['n_gpus'], json.loads(l)['regimes']['hetero_c4']['result_checksum'], json.loads(l)['regimes']['hetero_c4']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
     rank2c5) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2c5 500 python bench.py --gpus 2 --sections c5 --no-cpu-baseline && run rank1c5 300 python bench.py --sections c5 --no-cpu-baseline && grep -h result_checksum gpurun_out/rank2c5.log gpurun_out/rank1c5.log | python -c "import sys, json; [print(json.loads(l)['n_gpus'], json.loads(l)['regimes']['c5_hetero']['result_checksum'], json.loads(l)['regimes']['c5_hetero']['ms_per_job']) for l in sys.stdin if l.startswith('{')]" ;;
