@@ -501,22 +501,30 @@ def headline(args, dev, world, rank, workload="c2"):
                 engine.shap_kernel(d["bits"], S, out=d["k"], scratch=d["cnt"])
                 d["fit"].prepare(d["bits"], d["y"][:, 0], d["k"], w0[f0:f1])
 
+            prod_ev = torch.cuda.Event()
+
             def pipe_step(i_set, row):
+                # the fit's Adam steps alone are the chain: the next repeat's production, and
+                # this fit's losses / best epoch / status and its mean / std (or staging copy)
+                # run on s1; the next fit waits only for its production (prod_ev)
                 cur = torch.cuda.current_stream()
-                s1.wait_stream(cur)
+                s1.wait_stream(cur)  # the production rewrites the set the previous fit used
                 d = sets[i_set]
-                w = d["fit"].fit(d["bits"], d["k"])
+                w = d["fit"].fit_steps(d["bits"], d["k"])
                 out = None
-                if row is None:
-                    out = part_c(w)
-                else:
-                    row[ow:ow + nf * S * 4].view(torch.float32).copy_(w.reshape(-1))
                 with torch.cuda.stream(s1):
                     if row is not None:  # this step's repeat: logits + kernel weights
                         row[oy:oy + nl * 4].view(torch.float32).copy_(d["y"][:, 0])
                         row[ok_:ok_ + nl * 8].view(torch.float64).copy_(d["k"])
                     produce(sets[1 - i_set])
-                cur.wait_stream(s1)
+                    prod_ev.record(s1)
+                    s1.wait_stream(cur)  # after this fit's steps
+                    d["fit"].finish(d["k"])
+                    if row is None:
+                        out = part_c(w)
+                    else:
+                        row[ow:ow + nf * S * 4].view(torch.float32).copy_(w.reshape(-1))
+                cur.wait_event(prod_ev)
                 return out
 
             def stacked(b):  # mean / std over all ranks' repeats of replay buffer b's U steps
@@ -533,6 +541,7 @@ def headline(args, dev, world, rank, workload="c2"):
                 with engine.capture_guard(), torch.cuda.graph(gph):
                     for j in range(unroll):
                         outs.append(pipe_step((b * unroll + j) & 1, stage[b][j] if ex else None))
+                    torch.cuda.current_stream().wait_stream(s1)  # join the side stream
                 graphs.append((gph, outs))
 
             def exchange(b):
@@ -653,7 +662,10 @@ def headline(args, dev, world, rank, workload="c2"):
                               "replay, XPG_BENCH_UNROLL): step i's surrogate "
                               "fit runs beside step i+1's masks -> forward + KernelSHAP "
                               "(double-buffered; the fit's prologue kernel runs with the "
-                              "production; prologue untimed, K fits + K productions timed)"
+                              "production, its losses / best epoch and the mean / std after "
+                              "its Adam steps on the side stream, so consecutive fits' steps "
+                              "run back to back; prologue untimed, K fits + K productions "
+                              "timed)"
                               if pipe else "one captured HIP graph replayed per step") +
                               " (device-resident sampler seed advanced inside the graph); "
                               "phases_ms from eager steps")},

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -99,6 +99,10 @@ _SIGS = {
                          c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
     "xpg_wlm_fit_prepared": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, ctypes.POINTER(WlmParams), c_vp,
                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
+    "xpg_wlm_fit_steps": ([c_i64, c_vp, c_i64, c_i64, c_i64, c_vp, ctypes.POINTER(WlmParams), c_vp, c_vp,
+                           c_vp, c_vp, ctypes.c_size_t, c_vp], c_i32),
+    "xpg_wlm_fit_losses": ([c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.POINTER(WlmParams), c_vp, c_vp, c_vp,
+                            c_vp, ctypes.c_size_t, c_vp], c_i32),
     "xpg_khop_workspace": ([c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)], c_i32),
     "xpg_khop_subgraph": ([c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                            ctypes.c_size_t, c_vp], c_i32),

@@ -6123,7 +6123,7 @@ static int wlm_launch_prep(int64_t n_fits, const uint32_t* bits, int64_t rows, i
 static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                           const double* kernel, const xpg_wlm_params* params, float* w, float* adam_m, float* adam_v,
                           double* losses, int32_t* best_epoch, int32_t* status, char* ws, const WlmWs& L,
-                          hipStream_t st);
+                          hipStream_t st, int which = 3);
 
 int xpg_wlm_prepare(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                     const float* y, const double* kernel, const xpg_wlm_params* params, const float* w0,
@@ -6154,6 +6154,36 @@ int xpg_wlm_fit_prepared(int64_t n_fits, const uint32_t* bits, int64_t rows, int
   XPG_REQ(!L.grid, "wlm_fit_prepared: this shape takes the grid fit; use xpg_wlm_fit_from");
   return wlm_launch_fit(n_fits, bits, rows, cols, batch, kernel, params, w, adam_m, adam_v, losses, best_epoch,
                         status, static_cast<char*>(workspace), L, S(stream));
+}
+
+static int wlm_prepared_part(int which, int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols,
+                             int64_t batch, const double* kernel, const xpg_wlm_params* params, float* w,
+                             float* adam_m, float* adam_v, double* losses, int32_t* best_epoch, int32_t* status,
+                             void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
+  XPG_REQ(params != nullptr, "wlm_fit: params required");
+  XPG_REQ(n_fits <= 65535, "wlm_fit: at most 65535 fits per launch");
+  WlmWs L;
+  int rc = wlm_layout(n_fits, rows, cols, batch, &L);
+  if (rc) return rc;
+  XPG_REQ(workspace_bytes >= L.total, "wlm_fit: workspace too small");
+  XPG_REQ(!L.grid, "wlm_fit_steps / wlm_fit_losses: this shape takes the grid fit; use xpg_wlm_fit_from");
+  return wlm_launch_fit(n_fits, bits, rows, cols, batch, kernel, params, w, adam_m, adam_v, losses, best_epoch,
+                        status, static_cast<char*>(workspace), L, S(stream), which);
+}
+
+int xpg_wlm_fit_steps(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                      const double* kernel, const xpg_wlm_params* params, float* w, float* adam_m, float* adam_v,
+                      void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
+  return wlm_prepared_part(1, n_fits, bits, rows, cols, batch, kernel, params, w, adam_m, adam_v, nullptr, nullptr,
+                           nullptr, workspace, workspace_bytes, stream);
+}
+
+int xpg_wlm_fit_losses(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, const double* kernel,
+                       const xpg_wlm_params* params, double* losses, int32_t* best_epoch, int32_t* status,
+                       void* workspace, size_t workspace_bytes, xpg_stream_t stream) {
+  XPG_REQ(losses && best_epoch, "wlm_fit_losses: losses and best_epoch required");
+  return wlm_prepared_part(2, n_fits, nullptr, rows, cols, batch, kernel, params, nullptr, nullptr, nullptr, losses,
+                           best_epoch, status, workspace, workspace_bytes, stream);
 }
 
 int xpg_wlm_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
@@ -6230,10 +6260,12 @@ static int wlm_launch_prep(int64_t n_fits, const uint32_t* bits, int64_t rows, i
 
 // the fit proper (multi-workgroup or one-workgroup kernel) + losses / best epoch / status, on a
 // workspace k_wlm_prep has prepared
+// which: 1 = the Adam steps (fit kernel), 2 = losses / best epoch / status (k_wlm_loss_best),
+// 3 = both in stream order
 static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
                           const double* kernel, const xpg_wlm_params* params, float* w, float* adam_m, float* adam_v,
                           double* losses, int32_t* best_epoch, int32_t* status, char* ws, const WlmWs& L,
-                          hipStream_t st) {
+                          hipStream_t st, int which) {
   WlmStep* stp = reinterpret_cast<WlmStep*>(ws + L.steps_off);
   uint32_t* colbits = reinterpret_cast<uint32_t*>(ws + L.colbits_off);
   float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
@@ -6243,9 +6275,11 @@ static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, in
   const int words = words_of(cols);
   const int ic = static_cast<int>(cols), ib = static_cast<int>(batch);
   const unsigned nf = static_cast<unsigned>(n_fits);
-  bool launched = false;
-  const uint32_t* errw = nullptr;
-  if (L.mc) {
+  bool launched = (which & 1) == 0;
+  // the multi-workgroup exchange's error word (nonzero: a partner's poll timed out, the weights
+  // are invalid) reaches the caller's status through k_wlm_loss_best
+  const uint32_t* errw = L.mc ? reinterpret_cast<uint32_t*>(ws + L.cnt_off) + n_fits : nullptr;
+  if (L.mc && (which & 1)) {
     uint32_t* cnt = reinterpret_cast<uint32_t*>(ws + L.cnt_off);
     uint64_t* xp = reinterpret_cast<uint64_t*>(ws + L.xp_off);
     // granule tags carry a per-call epoch (stale cache lines of earlier calls never match)
@@ -6276,9 +6310,6 @@ static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, in
     XPG_WLM_MC(4, 1) XPG_WLM_MC(4, 2) XPG_WLM_MC(4, 4)
 #undef XPG_WLM_MC
     if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported slice width");
-    // the exchange's error word (nonzero: a partner's poll timed out, the weights are invalid)
-    // reaches the caller's status through k_wlm_loss_best
-    errw = cnt + n_fits;
   }
   const int cpt = static_cast<int>(cdiv(cols, 1024));
 #define XPG_WLM(C, TL)                                                                                     \
@@ -6294,6 +6325,7 @@ static int wlm_launch_fit(int64_t n_fits, const uint32_t* bits, int64_t rows, in
   XPG_WLM(1, false) XPG_WLM(2, false) XPG_WLM(4, false) XPG_WLM(8, false) XPG_WLM(16, false)
 #undef XPG_WLM
   if (!launched) return fail(XPG_EINVAL, "wlm_fit: unsupported column count");
+  if (!(which & 2)) return XPG_OK;
   // one launch: every step's loss and the first best epoch (+ the exchange status word)
   hipLaunchKernelGGL(k_wlm_loss_best, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, p_hist, w_hist,
                      kernel, stp, rows, ic, ib, params->l1_lambda, losses, best_epoch,

@@ -773,6 +773,28 @@ class PreparedFit:
              ptr(self.ws), self.ws.numel(), _lib.stream_of(bits.device))
         return self.w
 
+    def fit_steps(self, bits, kernel):
+        """`fit` without its losses / best epoch / status launch (xpg_wlm_fit_steps, ABI v17):
+        only the Adam steps on the current stream; call `losses` afterwards (any stream ordered
+        after this one) before the workspace is prepared again."""
+        F, R, S, B = self.shape
+        self._check("bits", bits, torch.int32, F * R * words_of(S))
+        self._check("kernel", kernel, torch.float64, F * R)
+        call("xpg_wlm_fit_steps", F, ptr(bits), R, S, B, ptr(kernel), ctypes.byref(self.p),
+             ptr(self.w), ptr(self.m), ptr(self.v), ptr(self.ws), self.ws.numel(),
+             _lib.stream_of(bits.device))
+        return self.w
+
+    def finish(self, kernel):
+        """The losses, first best epoch and status word of the last `fit_steps`
+        (xpg_wlm_fit_losses) on the current stream."""
+        F, R, S, B = self.shape
+        self._check("kernel", kernel, torch.float64, F * R)
+        call("xpg_wlm_fit_losses", F, R, S, B, ptr(kernel), ctypes.byref(self.p), ptr(self.losses),
+             ptr(self.best), ptr(self.status), ptr(self.ws), self.ws.numel(),
+             _lib.stream_of(kernel.device))
+        return self.losses, self.best
+
 
 def wlm_fit(bits, cols, batch, y, kernel, w0, params, m0=None, v0=None, step0=0, check=True,
             status=None):

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 16
+#define XPG_ABI_VERSION 17
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -293,6 +293,17 @@ int xpg_wlm_fit_prepared(int64_t n_fits, const uint32_t* bits, int64_t rows, int
                          float* w, float* adam_m, float* adam_v, double* losses,
                          int32_t* best_epoch, int32_t* status, void* workspace,
                          size_t workspace_bytes, xpg_stream_t stream);
+
+/* xpg_wlm_fit_prepared in its two launches (v17): the Adam steps (the fit kernel: w, adam_m,
+ * adam_v) and then, in stream order after them, the losses / first best epoch / status word
+ * (k_wlm_loss_best).  A caller that needs the next fit to start right after this one's steps can
+ * put the losses on another stream (after an event on the steps' stream). */
+int xpg_wlm_fit_steps(int64_t n_fits, const uint32_t* bits, int64_t rows, int64_t cols, int64_t batch,
+                      const double* kernel, const xpg_wlm_params* params, float* w, float* adam_m,
+                      float* adam_v, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
+int xpg_wlm_fit_losses(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, const double* kernel,
+                       const xpg_wlm_params* params, double* losses, int32_t* best_epoch,
+                       int32_t* status, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
 
 /* ---------------------------------------------------------------- k-hop computational subgraph */
 /* Replaces Data.comp_graph's PyG k_hop_subgraph(seed, hops, edge_index, relabel_nodes=True,

@@ -394,7 +394,8 @@ def test_masked_forward_vs_oracle_fp64(fwd_path):
 def test_prepared_fit_equals_fit_from(S, R, B):
     """xpg_wlm_prepare + xpg_wlm_fit_prepared (engine.PreparedFit) == xpg_wlm_fit_from bit for
     bit (w, losses, best epoch), twice on the same instance (the second prepare resets w / m / v
-    and the exchange slots), and two instances interleaved as the pipelined bench uses them."""
+    and the exchange slots; the second time as xpg_wlm_fit_steps + xpg_wlm_fit_losses, the
+    losses on another stream), and two instances interleaved as the pipelined bench uses them."""
     e = _eng()
     params = {"lr": 0.01, "l1_lambda": 1e-4}
     g = torch.Generator().manual_seed(S)
@@ -411,7 +412,15 @@ def test_prepared_fit_equals_fit_from(S, R, B):
         for i, (bits, y, k, w0, ref) in enumerate(fits):
             pf[i].prepare(bits, y, k, w0)
         for i, (bits, y, k, w0, ref) in enumerate(fits):
-            w = pf[i].fit(bits, k)
+            if rep == 0:
+                w = pf[i].fit(bits, k)
+            else:  # the split launches (ABI v17): steps, then losses on a second stream
+                w = pf[i].fit_steps(bits, k)
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    pf[i].finish(k)
+                torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
             e.check_fit_status(pf[i].status)
             assert torch.equal(w, ref[0]), (rep, i)
@@ -447,16 +456,21 @@ def test_pipelined_prepared_fits_equal_eager():
         e.shap_kernel(d["bits"], S, out=d["k"], scratch=d["cnt"])
         d["fit"].prepare(d["bits"], d["y"][:, 0], d["k"], w0)
 
-    def pipe_step(i, snap):
+    prod_ev = torch.cuda.Event()
+
+    def pipe_step(i, snap):  # bench.py's form: the fit's losses and outputs on the side stream
         cur = torch.cuda.current_stream()
         s1.wait_stream(cur)
         d = sets[i]
-        w = d["fit"].fit(d["bits"], d["k"])
-        snap[0].copy_(w)
-        snap[1].copy_(d["fit"].losses)
+        w = d["fit"].fit_steps(d["bits"], d["k"])
         with torch.cuda.stream(s1):
             produce(sets[1 - i])
-        cur.wait_stream(s1)
+            prod_ev.record(s1)
+            s1.wait_stream(cur)
+            d["fit"].finish(d["k"])
+            snap[0].copy_(w)
+            snap[1].copy_(d["fit"].losses)
+        cur.wait_event(prod_ev)
 
     produce(sets[0])  # prologue: seed 700
     torch.cuda.synchronize()
@@ -464,6 +478,7 @@ def test_pipelined_prepared_fits_equal_eager():
     with _eng().capture_guard(), torch.cuda.graph(g):
         for j in range(2):
             pipe_step(j, snaps[j])
+        torch.cuda.current_stream().wait_stream(s1)
     for rep in range(3):
         g.replay()
         torch.cuda.synchronize()
