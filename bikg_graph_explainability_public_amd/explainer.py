@@ -10,6 +10,7 @@ DataFrames) follows the reference step by step; the per-repeat hot path runs on 
 Repeats draw masks and the surrogate's initial weights from torch's CPU generator in the
 reference's order (compat sampler), so results match the reference CPU path for the same seed.
 """
+import operator
 import random
 import time
 import warnings
@@ -214,8 +215,9 @@ class Explainer:
         except AssertionError:
             return False
         if c["pos"] is not None:
-            from .data import take_names
-            return take_names(self.names, c["pos"]) == c["sub_names"]
+            # the subgraph's name objects at their positions, compared as a tuple (identity
+            # first, then ==): ~10 us at S = 1.2k instead of re-deriving the str forms (0.3 ms)
+            return _pick(self.names, c["pos"]) == c["pos_names"]
         return True
 
     def clear_cache(self):
@@ -311,7 +313,9 @@ class Explainer:
                 "sub_ind": sub_ind, "sub_nt": sub_nt, "sub_et": sub_et, "h_ntypes": h_ntypes,
                 "h_etypes": h_etypes, "padded_dims": padded_dims, "sub_pw": sub_pw,
                 "sub_pw_names": sub_pw_names, "sub_pw_inds": sub_pw_inds, "S": S,
-                "has_pathways": pathways is not None, "ind": ind, "pos": pos}
+                "has_pathways": pathways is not None, "ind": ind,
+                "pos": tuple(pos.tolist()) if pos is not None else None,
+                "pos_names": _pick(names, tuple(pos.tolist())) if pos is not None else None}
 
     def run(self, element, times=1):
         """explainer.py:316-546."""
@@ -673,6 +677,16 @@ def _is_member(element, names, idx):
     if i is None:
         return False
     return names[i] == element or element in names
+
+
+def _pick(names, pos):
+    """The name objects at positions `pos` (a tuple of ints) as a tuple (tuples of atoms leave
+    the cyclic collector's lists; a list of S ints would stay tracked)."""
+    if not pos:
+        return ()
+    if len(pos) == 1:
+        return (names[pos[0]],)
+    return operator.itemgetter(*pos)(names)
 
 
 def _snapshot(x):
