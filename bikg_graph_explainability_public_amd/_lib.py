@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -70,6 +70,7 @@ _SIGS = {
     "xpg_sample_shapley": ([ctypes.c_uint64, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),
     "xpg_sample_shapley_counts": ([ctypes.c_uint64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp], c_i32),
     "xpg_sample_shapley_dev": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),
+    "xpg_sample_shapley_sets": ([c_vp, c_i32, c_i64, c_i64, c_vp, c_vp], c_i32),
     "xpg_mt19937_mask_bits": ([c_vp, c_vp, c_vp, c_i64, c_i64, c_vp], c_i32),
     "xpg_mt19937_community_bits": ([c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i64,
                                     c_vp], c_i32),
@@ -158,5 +159,14 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(device=None):
+    """The current HIP stream of `device` (a torch.device, or None = the current device) as a
+    handle.  Read as torch's raw stream pointer: building a torch.cuda.Stream object per native
+    call cost ~9 us of host time each."""
+    if _raw_stream is not None:
+        idx = device.index if isinstance(device, torch.device) else None
+        return ctypes.c_void_p(_raw_stream(torch.cuda.current_device() if idx is None else idx))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

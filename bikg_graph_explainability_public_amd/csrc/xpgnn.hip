@@ -5601,6 +5601,18 @@ int xpg_sample_shapley_dev(const uint64_t* seed, int64_t row_offset, int64_t row
   return launch_shapley(0, row_offset, rows, cols, bits, nullptr, S(stream), seed);
 }
 
+int xpg_sample_shapley_sets(const uint64_t* seeds, int32_t n_sets, int64_t rows, int64_t cols, uint32_t* bits,
+                            xpg_stream_t stream) {
+  XPG_REQ(seeds && n_sets >= 0 && rows >= 0 && cols > 0 && (bits || n_sets == 0 || rows == 0),
+          "shapley sets: bad shape");
+  const int64_t set_words = rows * ((cols + 31) / 32);
+  for (int32_t k = 0; k < n_sets; ++k) {
+    const int rc = launch_shapley(seeds[k], 0, rows, cols, bits + k * set_words, nullptr, S(stream));
+    if (rc != XPG_OK) return rc;
+  }
+  return XPG_OK;
+}
+
 int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols, uint32_t* bits,
                               int32_t* counts, xpg_stream_t stream) {
   XPG_REQ(rows >= 0 && cols > 0 && row_offset >= 0 && counts, "shapley: bad shape");

@@ -9,6 +9,7 @@
   only; no CPU fallback).  The engine path never materialises the B-fold union graph at all.
 """
 import itertools
+import operator
 
 import numpy as np
 import torch
@@ -51,7 +52,8 @@ def take_names(names, idx):
     if not len(idx):
         return []
     ii = idx.tolist() if hasattr(idx, "tolist") else [int(i) for i in idx]  # one host copy
-    return np.array([names[i] for i in ii], dtype=str).tolist()
+    picked = (names[ii[0]],) if len(ii) == 1 else operator.itemgetter(*ii)(names)
+    return np.array(picked, dtype=str).tolist()
 
 
 def pad_feat_tensors(feat_tensors):
@@ -147,7 +149,7 @@ class Data:
         hops = n_hops + 1
         n = self.feat.shape[0]
         subset, sub_ei, sub_ind, emask = k_hop_subgraph(ind, hops, self.edge_index, n)
-        if int(emask.sum()) == 0:
+        if sub_ei.shape[1] == 0:  # no kept edge (sub_ei has one column per kept edge)
             sub_ei = torch.tensor([[int(sub_ind)], [int(sub_ind)]], dtype=torch.long,
                                   device=self.edge_index.device)
         sub_feat = self.feat[subset]
@@ -243,6 +245,6 @@ class Data:
     @staticmethod
     def config_val_dataframe(config_val_mean, config_val_std, names):
         """data.py:651-693."""
-        return sorted_frame(names, {"config_value_mean": config_val_mean.detach().cpu().numpy(),
-                                    "config_value_std": config_val_std.detach().cpu().numpy()},
+        ms = torch.stack([config_val_mean.detach(), config_val_std.detach()]).cpu().numpy()
+        return sorted_frame(names, {"config_value_mean": ms[0], "config_value_std": ms[1]},
                             "config_value_mean")

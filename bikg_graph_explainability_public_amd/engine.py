@@ -89,6 +89,16 @@ def sample_shapley(seed: int, rows: int, cols: int, device, row_offset: int = 0,
     return bits, counts
 
 
+def sample_shapley_sets(seeds, rows: int, cols: int, device):
+    """len(seeds) independent `sample_shapley(seed, rows, cols)` draws as one [n, rows, words]
+    tensor, in one native call (Explainer.run's repeats)."""
+    n = len(seeds)
+    bits = torch.empty((n, rows, words_of(cols)), dtype=torch.int32, device=device)
+    arr = (ctypes.c_uint64 * max(n, 1))(*[int(s) & (2 ** 64 - 1) for s in seeds])
+    call("xpg_sample_shapley_sets", arr, n, rows, cols, ptr(bits), _lib.stream_of(torch.device(device)))
+    return bits
+
+
 # torch.get_rng_state() of the CPU generator (at::CPUGeneratorImplState, legacy POD first):
 # uint64 the_initial_seed | int32 left | int32 seeded | uint64 next | uint64 state[624] | ...
 _RNG_LEFT, _RNG_NEXT, _RNG_STATE = 8, 16, 24
@@ -545,8 +555,12 @@ class ForwardPlan:
                 self._i32(ld, "self_ptr", lay["self_ptr"])
                 self._i32(ld, "self_eid", nz(lay["self_eid"]))
             n_types = program.n_types
-            bias = torch.zeros((n_types, f_out_pad), dtype=torch.float32, device=device)
-            bias[:, :conv.f_out] = conv.bias.to(device).reshape(-1, conv.f_out)
+
+            def make_bias(conv=conv, f_out_pad=f_out_pad):
+                b = torch.zeros((n_types, f_out_pad), dtype=torch.float32, device=device)
+                b[:, :conv.f_out] = conv.bias.to(device).reshape(-1, conv.f_out)
+                return b
+            bias = self._program_tensor(program, ("bias", li), make_bias)
             self._keep.append(bias)
             ld.bias = bias.data_ptr()
             ld.n_types = n_types
@@ -567,10 +581,13 @@ class ForwardPlan:
                     ld.terms[k].table = Tp.data_ptr()
                 ld.weight = None
             else:
-                kt = len(terms) * prev_pad
-                Wc = torch.zeros((f_out_pad, kt), dtype=torch.float32, device=device)
-                for k, term in enumerate(terms):
-                    Wc[:conv.f_out, k * prev_pad:k * prev_pad + conv.f_in] = term.weight.to(device)
+                def make_wc(conv=conv, terms=terms, prev_pad=prev_pad, f_out_pad=f_out_pad):
+                    w = torch.zeros((f_out_pad, len(terms) * prev_pad), dtype=torch.float32,
+                                    device=device)
+                    for k, term in enumerate(terms):
+                        w[:conv.f_out, k * prev_pad:k * prev_pad + conv.f_in] = term.weight.to(device)
+                    return w
+                Wc = self._program_tensor(program, ("wc", li, tuple(id(t) for t in terms)), make_wc)
                 self._keep.append(Wc)
                 ld.weight = Wc.data_ptr()
             prev_pad = f_out_pad
@@ -581,11 +598,14 @@ class ForwardPlan:
             n_pad = _rup(n_real, 32)
             if n_pad > 256:
                 raise ValueError("head layer wider than 256 is not supported")
-            Wp = torch.zeros((n_pad, prev_pad), dtype=torch.float32, device=device)
-            Wp[:n_real, :k_real] = h.weight.to(device)
-            bp = torch.zeros(n_pad, dtype=torch.float32, device=device)
-            if h.bias is not None:
-                bp[:n_real] = h.bias.to(device)
+            def make_head(h=h, n_real=n_real, k_real=k_real, n_pad=n_pad, prev_pad=prev_pad):
+                w = torch.zeros((n_pad, prev_pad), dtype=torch.float32, device=device)
+                w[:n_real, :k_real] = h.weight.to(device)
+                b = torch.zeros(n_pad, dtype=torch.float32, device=device)
+                if h.bias is not None:
+                    b[:n_real] = h.bias.to(device)
+                return w, b
+            Wp, bp = self._program_tensor(program, ("head", i), make_head)
             self._keep += [Wp, bp]
             hd = self._head[i]
             hd.k_pad, hd.n_real, hd.n_pad, hd.act = prev_pad, n_real, n_pad, ACT[h.act]
@@ -614,6 +634,17 @@ class ForwardPlan:
             self.n_out = 1
         self._upload_i32()
         self._ws = None
+
+    def _program_tensor(self, program, key, make):
+        """Device tensors derived from the program's weights alone (padded biases, the stacked
+        dense weights of layers >= 1, head layers): built once per (program, device) and shared by
+        every plan of that program (pipeline.compiled_program reuses a program while the module's
+        parameters are unchanged), so a new query's plan only builds its own arrays and tables."""
+        cache = program.__dict__.setdefault("_device_tensors", {})
+        k = (str(self.device),) + key
+        if k not in cache:
+            cache[k] = make()
+        return cache[k]
 
     def _i32(self, obj, field, a):
         """Stage an int32 array for descriptor field `obj.field`; `_upload_i32` moves every

@@ -10,6 +10,7 @@ DataFrames) follows the reference step by step; the per-repeat hot path runs on 
 Repeats draw masks and the surrogate's initial weights from torch's CPU generator in the
 reference's order (compat sampler), so results match the reference CPU path for the same seed.
 """
+import collections.abc
 import operator
 import random
 import time
@@ -32,20 +33,21 @@ class PhaseClock:
     each mark (no synchronisation); `times()` synchronises once and returns, per phase, the
     host wall milliseconds and the device milliseconds between its two events."""
 
-    def __init__(self):
+    def __init__(self, stream=None):
         self.marks = []
+        self.stream = stream  # the run's stream (torch.cuda.current_stream() per mark: ~9 us)
 
     def mark(self, name):
         ev = None
-        if torch.cuda.is_available():
+        if self.stream is not None:
             ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
+            ev.record(self.stream)
         self.marks.append((name, time.perf_counter(), ev))
 
     def times(self):
         if len(self.marks) < 2:
             return {}
-        if torch.cuda.is_available():
+        if self.stream is not None:
             torch.cuda.synchronize()
         out = {}
         for (name, t0, e0), (_, t1, e1) in zip(self.marks, self.marks[1:]):
@@ -160,10 +162,22 @@ class Explainer:
 
     @staticmethod
     def weight_stacking(weights):
-        """explainer.py:288-314 — mean and population std over repeats (one fused reduction)."""
-        stack = torch.vstack(weights)
+        """explainer.py:288-314 — mean and population std over repeats (one fused reduction);
+        `weights` is the list of per-repeat weight tensors, or already their [times, S] stack."""
+        stack = weights if isinstance(weights, torch.Tensor) and weights.dim() == 2 else \
+            torch.vstack(weights)
         std, mean = torch.std_mean(stack, 0, unbiased=False)
         return mean, std
+
+    def _place_arch(self, device):
+        """self.arch.to(device).eval() (explainer.py:338-339), skipped when every module is
+        already in eval mode and every parameter / buffer on `device`: Module.to + eval walk the
+        module tree through _apply (~0.15 ms of host time per call); the check is ~20 us."""
+        mods = list(self.arch.modules())
+        if any(m.training for m in mods) or any(
+                t is not None and t.device != device
+                for m in mods for t in (*m._parameters.values(), *m._buffers.values())):
+            self.arch = self.arch.to(device).eval()
 
     def _verify_key(self, plan, c):
         """What the compiled program's check depends on: the module object, every parameter
@@ -323,15 +337,15 @@ class Explainer:
             raise _lib.NativeLibraryError("Explainer.run needs an MI355X (HIP) device; "
                                           "there is no CPU fallback")
         _lib.load()
-        clock = PhaseClock()
-        clock.mark("setup")
         device = torch.device("cuda", torch.cuda.current_device())
+        clock = PhaseClock(torch.cuda.current_stream(device))
+        clock.mark("setup")
         if times == 1:
             set_seed(self.params["seed"])
         # multi-GPU: every rank continues from rank 0's generator, so all ranks draw the same
         # masks / sampler seeds / initial weights (checked by checksum below)
         sharding.sync_rng(self.group)
-        self.arch = self.arch.to(device).eval()
+        self._place_arch(device)
         clock.mark("prepare")
         # a query explained again (same graph, names, module state) reuses its computational
         # subgraph, plan and arch check: prepare() and the plan build are the run's largest host
@@ -413,11 +427,10 @@ class Explainer:
             cmask = Mask(mfeat, sub_ei, c["sub_pw_inds"], self.params, mproblem)
             cplan = cmask.community_plan()
             ctabs = engine.community_tables(cplan, c["sub_pw_inds"], S, device)
+        seeds = []  # device Shapley sampler: every repeat's seed first, then one native call
         for _ in range(times):
             if on_device and c["sub_pw_inds"] is None:
-                R = int(self.params["interpret_samples"] * epochs)
-                seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-                bits_list.append(engine.sample_shapley(seed, R, S, device))
+                seeds.append(torch.randint(0, 2 ** 62, (1,)))  # read together below
                 masks.append(None)
             elif on_device:
                 seed = int(torch.randint(0, 2 ** 62, (1,)).item())
@@ -431,9 +444,14 @@ class Explainer:
                 masks.append(None)
             w0_list.append(LinearRegression.initial_weights(S))
             dataloader_seed_draw()
-        R = bits_list[0].shape[0]
+        if seeds:
+            seeds = torch.cat(seeds).tolist()
+            bits = engine.sample_shapley_sets(seeds, int(self.params["interpret_samples"] * epochs),
+                                              S, device)       # [times, R, W]
+        else:
+            bits = torch.stack(bits_list)                   # [times, R, W]
+        R = bits.shape[1]
         batch = R // epochs
-        bits = torch.stack(bits_list)                       # [times, R, W]
         # multi-GPU (torch.distributed initialised, one process per GPU): rows of the forward /
         # KernelSHAP and whole surrogate fits are sharded over ranks, outputs all-gathered, so
         # every rank returns the single-GPU result (sharding.py).
@@ -467,7 +485,7 @@ class Explainer:
             def generic(t0, t1):
                 ys = [pipeline.generic_edge_outputs(
                     self.arch, sub_feat, sub_ei,
-                    engine.unpack_masks(bits_list[i], S) if masks[i] is None else masks[i],
+                    engine.unpack_masks(bits[i], S) if masks[i] is None else masks[i],
                     *c["link"], max_rows=batch) for i in range(t0, t1)]
                 return torch.stack(ys) if ys else torch.empty((0, R), device=device)
             y = sharding.gather_map(times, generic, g)
@@ -475,7 +493,7 @@ class Explainer:
             def generic(t0, t1):
                 ys = [pipeline.generic_outputs(
                     self.arch, sub_feat, sub_ei,
-                    engine.unpack_masks(bits_list[i], S) if masks[i] is None else masks[i],
+                    engine.unpack_masks(bits[i], S) if masks[i] is None else masks[i],
                     sub_ind, self.problem, *geo, batch=batch, q4=q4) for i in range(t0, t1)]
                 return torch.stack(ys) if ys else torch.empty((0, R), device=device)
             y = sharding.gather_map(times, generic, g)
@@ -499,12 +517,10 @@ class Explainer:
         w = sharding.gather_map(times, fit, g)
         losses = sharding.gather_rows(fits["losses"], times, g)
         best = sharding.gather_rows(fits["best"], times, g)
-        config_vals = [w[i] for i in range(times)]
-        diag = [{"losses": losses[i], "best_epoch": best[i], "rows": R, "batch": batch,
-                 "y": y[i], "bits": bits[i], "kernel": kern[i], "w0": w0_list[i]}
-                for i in range(times)]
+        diag = _Repeats(losses=losses, best_epoch=best, rows=R, batch=batch, y=y, bits=bits,
+                        kernel=kern, w0=w0_list)
         clock.mark("output")
-        mean, std = self.weight_stacking(config_vals)
+        mean, std = self.weight_stacking(w)
         config_val_df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
         pathway_df = None
         if c["has_pathways"]:
@@ -514,7 +530,7 @@ class Explainer:
         if qkey is not None:
             self._trim_cache(qkey)
         self.last_run = {"engine": plan is not None, "repeats": diag, "S": S,
-                         "sub_ind": sub_ind, "plan": plan, "weights": config_vals,
+                         "sub_ind": sub_ind, "plan": plan, "weights": w.unbind(0),
                          "phases": clock, "arch_check": arch_check,
                          "query_cache": "off" if qkey is None else "hit" if hit else "miss"}
         return config_val_df, pathway_df
@@ -546,7 +562,7 @@ class Explainer:
             set_seed(self.params["seed"])
         g = self.group
         sharding.sync_rng(g)
-        self.arch = self.arch.to(device).eval()
+        self._place_arch(device)
         c = self.prepare(elements[0], device)
         # graph_prediction: every query indexes the same (whole) graph, so only the element
         # lookup of `prepare` differs per query (explainer.py:427-447)
@@ -624,7 +640,7 @@ class Explainer:
         out = []
         for q in range(Q):
             w = fitted[q]
-            mean, std = self.weight_stacking([w[i] for i in range(times)])
+            mean, std = self.weight_stacking(w)
             df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
             pdf = None
             if c["has_pathways"]:
@@ -634,6 +650,26 @@ class Explainer:
                          "bits": bits, "y": y, "kernel": kern, "w0": w0_all.reshape(Q, times, S),
                          "weights": fitted, "plan": plan}
         return out
+
+
+class _Repeats(collections.abc.Sequence):
+    """last_run["repeats"]: per repeat i a dict of its losses, best epoch, rows, batch, forward
+    outputs y, mask bits, KernelSHAP weights and initial surrogate weights, built when asked for
+    (the run keeps the stacked tensors; 60 tensor views per times=10 call cost ~0.16 ms)."""
+
+    def __init__(self, rows, batch, **stacked):
+        self._rows, self._batch, self._t = rows, batch, stacked
+
+    def __len__(self):
+        return len(self._t["w0"])
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        t = self._t
+        return {"losses": t["losses"][i], "best_epoch": t["best_epoch"][i], "rows": self._rows,
+                "batch": self._batch, "y": t["y"][i], "bits": t["bits"][i],
+                "kernel": t["kernel"][i], "w0": t["w0"][i]}
 
 
 _NAME_INDEX = {}

@@ -9,7 +9,9 @@ Architectures the engine cannot compile run through `generic_outputs` (the user'
 on the B-fold union graph built with the HIP edge-keep kernel) — still on the GPU, with the
 KernelSHAP and surrogate stages unchanged.
 """
+import collections
 import warnings
+import weakref
 
 import torch
 
@@ -30,6 +32,31 @@ def relation_edges(edge_index, edge_type, n_rel):
     return [edge_index[:, et == r] for r in range(n_rel)]
 
 
+_PROGRAMS = collections.OrderedDict()  # compiled_program's cache: key -> (weakref(arch), program)
+
+
+def compiled_program(arch, edge_type_names=None, node_type_names=None):
+    """compile_arch(arch, ...) once per module state: keyed by the module (identity, checked by
+    weak reference), every parameter and buffer (storage + in-place version counter: an
+    optimizer step, load_state_dict or a replaced tensor compiles again) and the type names.
+    The program carries the plans' weight-derived device tensors (ForwardPlan._program_tensor),
+    so a new query's plan neither lowers the module nor re-pads its weights.  8 programs kept."""
+    state = tuple((t.data_ptr(), t._version) for t in arch.parameters()) + \
+        tuple((t.data_ptr(), t._version) for t in arch.buffers())
+    key = (id(arch), state,
+           tuple(tuple(e) for e in edge_type_names) if edge_type_names is not None else None,
+           tuple(node_type_names) if node_type_names is not None else None)
+    hit = _PROGRAMS.get(key)
+    if hit is not None and hit[0]() is arch:
+        _PROGRAMS.move_to_end(key)
+        return hit[1]
+    prog = compile_arch(arch, edge_type_names, node_type_names)
+    _PROGRAMS[key] = (weakref.ref(arch), prog)
+    while len(_PROGRAMS) > 8:
+        _PROGRAMS.popitem(last=False)
+    return prog
+
+
 def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
                node_type_names=None, edge_type_names=None, padded_dims=None):
     """ForwardPlan for `arch` on the (sub)graph, or None when the engine cannot run it.
@@ -43,8 +70,8 @@ def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
         len(torch.unique(node_type)) >= 2
     hetero = edge_type_names is not None and edge_type is not None
     try:
-        prog = compile_arch(arch, edge_type_names if hetero else None,
-                            node_type_names if multi else None)
+        prog = compiled_program(arch, edge_type_names if hetero else None,
+                                node_type_names if multi else None)
     except UnsupportedArch as e:
         warnings.warn(f"engine cannot compile arch ({e}); using the generic torch path")
         return None
@@ -78,7 +105,7 @@ def build_edge_plan(arch, feat, edge_index, u, v):
     columns = the subgraph's edges, output = the LinkModel decoder's score of edge (u, v).
     None when the engine cannot compile `arch` (generic torch path)."""
     try:
-        prog = compile_arch(arch)
+        prog = compiled_program(arch)
     except UnsupportedArch as e:
         warnings.warn(f"engine cannot compile arch ({e}); using the generic torch path")
         return None

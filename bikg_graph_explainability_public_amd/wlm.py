@@ -36,9 +36,15 @@ class LinearRegression(nn.Module):
         same torch CPU generator -- bit-identical values and generator state, without building
         a module per repeat (~35 us each)."""
         assert isinstance(num_elements, int)
-        w = torch.empty((1, int(num_elements)))
-        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
-        return w.reshape(-1)
+        n = int(num_elements)
+        if n == 0:
+            return torch.empty(0)
+        # kaiming_uniform_(a=sqrt(5)) on [1, n]: fan_in n, leaky_relu gain, bound sqrt(3) * std
+        # (the same float operations, so the same bound and the same uniform_ draws)
+        gain = math.sqrt(2.0 / (1 + math.sqrt(5) ** 2))
+        bound = math.sqrt(3.0) * (gain / math.sqrt(n))
+        with torch.no_grad():
+            return torch.empty(n).uniform_(-bound, bound)
 
 
 def model_updates(linear_model, loss, best_loss):

@@ -16,6 +16,7 @@
  *                                        wlm.py (DataLoader batches, masks.py:197-229)
  *   xpg_sample_shapley                 — Mask.shapley_mask           masks.py:231-260
  *   xpg_sample_shapley_dev             — same, device-resident seed (graph replays)
+ *   xpg_sample_shapley_sets            — same, one draw per repeat in one call
  *   xpg_sample_communities             — Mask.get_internal_mask / get_external_indices +
  *                                        Pathways.mask_generator (masks.py:81-194,
  *                                        pathways.py:234-385)
@@ -45,7 +46,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 17
+#define XPG_ABI_VERSION 18
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -76,6 +77,11 @@ int xpg_sample_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t 
  * the stream (v11). */
 int xpg_sample_shapley_dev(const uint64_t* seed, int64_t row_offset, int64_t rows, int64_t cols,
                            uint32_t* bits, xpg_stream_t stream);
+/* n_sets independent Shapley draws in one call: set k = xpg_sample_shapley(seeds[k], 0, rows, cols)
+ * written at bits + k * rows * ceil(cols/32) (bits = [n_sets][rows][words]); seeds is a HOST array.
+ * Explainer.run(times = n_sets) draws every repeat's masks this way (one host call, v18). */
+int xpg_sample_shapley_sets(const uint64_t* seeds, int32_t n_sets, int64_t rows, int64_t cols,
+                            uint32_t* bits, xpg_stream_t stream);
 /* HOST function (no GPU work): the reference's compat Shapley draw torch.randint(0, 2, (rows, cols),
  * dtype=torch.bool) on torch's CPU generator (masks.py:231-260), replayed from the generator's
  * at::mt19937 state (state[624] words, left, next as torch.get_rng_state() stores them) and

@@ -16,6 +16,7 @@ Reference semantics cited: data.py:331 / model.py:62-116 (no degree limit), mask
 pathways.py:387-429, explainer.py:490-532, wlm.py:132-278.
 """
 import contextlib
+import copy
 import os
 import socket
 import sys
@@ -594,6 +595,14 @@ def test_explainer_arch_check_cached_per_module_state():
     exp.params = dict(params, verify_arch="always")
     exp.run("9", 1)
     assert exp.last_run["arch_check"] == "verified"
+    # new parameter values in place: the cached program (pipeline.compiled_program) and its
+    # padded device weights are rebuilt; the result equals a fresh copy of the updated module's
+    exp.params = params
+    with torch.no_grad():
+        list(arch.parameters())[-1].add_(0.25)
+    df_m, _ = exp.run("9", 1)
+    df_c, _ = Explainer(feat.to(DEV), ei.to(DEV), copy.deepcopy(arch), params, names).run("9", 1)
+    assert df_m.equals(df_c) and not df_m.equals(df_b)
 
 
 def test_explainer_query_cache_same_results():

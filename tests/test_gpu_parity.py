@@ -124,6 +124,13 @@ def test_shapley_sampler_properties():
     assert torch.equal(part, a[1000:1100])
     c = e.sample_shapley(8, R, S, DEV)
     assert not torch.equal(a, c)
+    # one call per repeat set (Explainer.run): set k == sample_shapley(seeds[k]) bit for bit
+    seeds = [7, 2 ** 62 - 1, 8, 2 ** 64 - 5]
+    sets = e.sample_shapley_sets(seeds, 300, S, DEV)
+    assert sets.shape == (4, 300, (S + 31) // 32)
+    for k, s in enumerate(seeds):
+        assert torch.equal(sets[k], e.sample_shapley(s, 300, S, DEV))
+    assert e.sample_shapley_sets([], 300, S, DEV).shape == (0, 300, (S + 31) // 32)
 
 
 def test_shapley_sampler_device_seed_and_graph_replay():

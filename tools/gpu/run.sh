@@ -59,6 +59,8 @@ for step in "$@"; do
            run pmc_fetch_c3 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 && \
            run pmc_write_c3 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 ;;
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
+    apiprof3) run apiprof3 300 python -u tools/api_profile.py --graph c3 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+              run apitrace3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/apitrace3 -o run -- python3 tools/api_profile.py --graph c3 --top 5 ;;
     widetests) run widetests 600 python -u -m pytest tests/test_gpu_coverage.py tests/test_gpu_parity.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wide or c3 or hub" ;;
     idxab) run idxab 600 python -u tools/ws_ab.py --variants "${IDXAB:-B3=1,IDX=0;B3=1;B3=1,IDX=0;B3=1;B3=1,RP=6}" ;;
     probe) XPG_WLM=single run probe 120 ./tools/wlm_probe 1193 12800 256 && run probe_mc 120 ./tools/wlm_probe 1193 12800 256 ;;
