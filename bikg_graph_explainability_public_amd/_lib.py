@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -71,6 +71,9 @@ _SIGS = {
     "xpg_sample_shapley_counts": ([ctypes.c_uint64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp], c_i32),
     "xpg_sample_shapley_dev": ([c_vp, c_i64, c_i64, c_i64, c_vp, c_vp], c_i32),
     "xpg_sample_shapley_sets": ([c_vp, c_i32, c_i64, c_i64, c_vp, c_vp], c_i32),
+    "xpg_plan_arrays_build": ([c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp], c_i32),
+    "xpg_plan_arrays_take": ([c_vp, c_vp], c_i32),
+    "xpg_plan_arrays_free": ([c_vp], c_i32),
     "xpg_mt19937_mask_bits": ([c_vp, c_vp, c_vp, c_i64, c_i64, c_vp], c_i32),
     "xpg_mt19937_community_bits": ([c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i64,
                                     c_vp], c_i32),

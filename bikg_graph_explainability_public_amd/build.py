@@ -20,6 +20,7 @@ def hipcc():
 
 def build(force=False, verbose=True):
     deps = [SRC, os.path.join(HERE, "csrc", "khop.hip"), os.path.join(HERE, "csrc", "host_rng.h"),
+            os.path.join(HERE, "csrc", "plan_host.h"),
             os.path.join(os.path.dirname(HERE), "include", "xpgnn.h")]
     if not force and os.path.exists(OUT) and \
             all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):

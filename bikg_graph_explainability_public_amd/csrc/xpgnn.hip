@@ -23,6 +23,7 @@
 
 #include "../../include/xpgnn.h"
 #include "host_rng.h"
+#include "plan_host.h"
 
 namespace {
 
@@ -5552,6 +5553,63 @@ int xpg_mt19937_community_bits(uint32_t* state, int32_t* left, int32_t* next, in
   XPG_REQ(end == rows, "mt19937_community_bits: rows != the blocks' total");
   std::memset(bits, 0, sizeof(uint32_t) * static_cast<size_t>(rows) * static_cast<size_t>(words_of(cols)));
   hostrng::community_rows(state, left, next, cols, n_comm, comm_ptr, comm_cols, blocks, n_blocks, bits);
+  return XPG_OK;
+}
+
+int xpg_plan_arrays_build(int64_t S, int32_t n_rel, const int64_t* rel_ptr, const int64_t* src, const int64_t* dst,
+                          const int64_t* eid, const int64_t* queries, int64_t nq, int32_t L, void** handle,
+                          int64_t* sizes) {
+  XPG_REQ(handle && sizes && rel_ptr && queries && S > 0 && n_rel >= 0 && nq > 0 && L >= 1 && L <= 64,
+          "plan_arrays: bad arguments");
+  *handle = nullptr;
+  XPG_REQ(rel_ptr[0] == 0, "plan_arrays: rel_ptr[0] != 0");
+  for (int32_t r = 0; r < n_rel; ++r) XPG_REQ(rel_ptr[r + 1] >= rel_ptr[r], "plan_arrays: rel_ptr not monotone");
+  const int64_t E = rel_ptr[n_rel];
+  XPG_REQ(E == 0 || (src && dst), "plan_arrays: missing edges");
+  for (int64_t e = 0; e < E; ++e)
+    XPG_REQ(src[e] >= 0 && src[e] < S && dst[e] >= 0 && dst[e] < S, "plan_arrays: edge endpoint out of range");
+  {
+    std::vector<uint8_t> seen(S);
+    for (int64_t i = 0; i < nq; ++i) {
+      XPG_REQ(queries[i] >= 0 && queries[i] < S, "plan_arrays: query positions out of range");
+      XPG_REQ(!seen[queries[i]], "plan_arrays: duplicate query positions");
+      seen[queries[i]] = 1;
+    }
+  }
+  auto* A = new planhost::Arrays();
+  planhost::build(S, n_rel, rel_ptr, src, dst, eid, queries, nq, L, *A);
+  int64_t k = 0;
+  for (int32_t l = 0; l <= L; ++l) sizes[k++] = static_cast<int64_t>(A->fr[l].size());
+  auto put = [&](const planhost::Csr& c) {
+    for (const std::vector<int64_t>* v : {&c.ptr, &c.src, &c.eid, &c.smul, &c.sptr, &c.seid})
+      sizes[k++] = static_cast<int64_t>(v->size());
+  };
+  put(A->deg);
+  for (const planhost::Csr& c : A->lay) put(c);
+  *handle = A;
+  return XPG_OK;
+}
+
+int xpg_plan_arrays_take(void* handle, int64_t* out) {
+  XPG_REQ(handle && out, "plan_arrays_take: bad arguments");
+  auto* A = static_cast<planhost::Arrays*>(handle);
+  int64_t* o = out;
+  auto cp = [&](const std::vector<int64_t>& v) {
+    if (!v.empty()) std::memcpy(o, v.data(), sizeof(int64_t) * v.size());
+    o += v.size();
+  };
+  auto cp_csr = [&](const planhost::Csr& c) {
+    for (const std::vector<int64_t>* v : {&c.ptr, &c.src, &c.eid, &c.smul, &c.sptr, &c.seid}) cp(*v);
+  };
+  for (const auto& f : A->fr) cp(f);
+  cp_csr(A->deg);
+  for (const planhost::Csr& c : A->lay) cp_csr(c);
+  delete A;
+  return XPG_OK;
+}
+
+int xpg_plan_arrays_free(void* handle) {
+  delete static_cast<planhost::Arrays*>(handle);
   return XPG_OK;
 }
 

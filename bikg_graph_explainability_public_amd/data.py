@@ -53,6 +53,8 @@ def take_names(names, idx):
         return []
     ii = idx.tolist() if hasattr(idx, "tolist") else [int(i) for i in idx]  # one host copy
     picked = (names[ii[0]],) if len(ii) == 1 else operator.itemgetter(*ii)(names)
+    if set(map(type, picked)) == {str} and "\x00" not in "".join(picked):
+        return list(picked)  # str names: numpy's str conversion returns them unchanged
     return np.array(picked, dtype=str).tolist()
 
 

@@ -172,22 +172,31 @@ class Explainer:
     def _place_arch(self, device):
         """self.arch.to(device).eval() (explainer.py:338-339), skipped when every module is
         already in eval mode and every parameter / buffer on `device`: Module.to + eval walk the
-        module tree through _apply (~0.15 ms of host time per call); the check is ~20 us."""
+        module tree through _apply (~0.15 ms of host time per call); the check is ~20 us.
+        Returns the module's parameters and buffers (Module.parameters() / buffers() order, one
+        walk of the tree for the whole run) and their state: (storage, in-place version) each."""
         mods = list(self.arch.modules())
-        if any(m.training for m in mods) or any(
-                t is not None and t.device != device
-                for m in mods for t in (*m._parameters.values(), *m._buffers.values())):
-            self.arch = self.arch.to(device).eval()
+        params, bufs, seen = [], [], set()
+        for m in mods:
+            for group, out in ((m._parameters, params), (m._buffers, bufs)):
+                for t in group.values():
+                    if t is not None and id(t) not in seen:
+                        seen.add(id(t))
+                        out.append(t)
+        if any(m.training for m in mods) or any(t.device != device for t in params + bufs):
+            self.arch = self.arch.to(device).eval()  # same tensor objects, moved storage
+        state = (tuple((t.data_ptr(), t._version) for t in params),
+                 tuple((t.data_ptr(), t._version) for t in bufs))
+        return params, bufs, state
 
-    def _verify_key(self, plan, c):
+    def _verify_key(self, plan, c, state):
         """What the compiled program's check depends on: the module object, every parameter
-        and buffer (storage and in-place version counter: an optimizer step or load_state_dict
-        changes them), the plan kind, the graph's type structure and the plan's query-dependent
-        lowering (ForwardPlan drops other destination types' relation terms from a layer whose
-        targets share one node type, so two queries can lower the same module differently)."""
-        state = tuple((t.data_ptr(), t._version) for t in self.arch.parameters())
-        bufs = tuple((t.data_ptr(), t._version) for t in self.arch.buffers())
-        return (id(self.arch), state, bufs, self.edge_masks, bool(getattr(plan, "multi_type", False)),
+        and buffer (`state`: storage and in-place version counter: an optimizer step or
+        load_state_dict changes them), the plan kind, the graph's type structure and the plan's
+        query-dependent lowering (ForwardPlan drops other destination types' relation terms from a
+        layer whose targets share one node type, so two queries can lower the same module
+        differently)."""
+        return (id(self.arch), state[0], state[1], self.edge_masks, bool(getattr(plan, "multi_type", False)),
                 tuple(c["h_ntypes"] or ()), tuple(c["h_etypes"] or ()),
                 tuple(getattr(plan, "lowering", ())))
 
@@ -199,14 +208,14 @@ class Explainer:
         return (str(element), type(element).__name__, self.problem, self.edge_masks, str(device),
                 _freeze(self.element_type), str(self.params.get("verify_arch", True)))
 
-    def _query_sources(self):
+    def _query_sources(self, params, bufs):
         """Identity snapshot of what prepare() and the query's ForwardPlan read: the graph and
         type tensors (weak reference + storage + in-place version: a replaced tensor, even one
         the allocator put at the freed address, or an in-place edit never matches), the names /
         pathways inputs and the module (identity), the module's parameters and buffers."""
         return _snapshot((self.feat, self.edge_index, self.node_types, self.edge_types,
                           self.names, self.pathways, self.pathway_names, self.arch,
-                          tuple(self.arch.parameters()), tuple(self.arch.buffers())))
+                          tuple(params), tuple(bufs)))
 
     def _query_fingerprints(self):
         """Full-content fingerprints of the inputs read in full by prepare(): pathways and
@@ -242,12 +251,17 @@ class Explainer:
         """Keep the cache within params["plan_cache_bytes"] device bytes (default 2 GiB) and
         8 queries: oldest entries out first; the entry of the query just run always stays."""
         limit = int(self.params.get("plan_cache_bytes", 2 << 30))
-        user = _tensor_ptrs((self.feat, self.edge_index, self.node_types, self.edge_types))
+        user = None
 
-        def nbytes(e):
-            ctx = sum(t.numel() * t.element_size() for t in e["c"].values()
-                      if isinstance(t, torch.Tensor) and t.data_ptr() not in user)
-            return ctx + (e["plan"].device_bytes() if e["plan"] is not None else 0)
+        def nbytes(e):  # once per entry (an entry's tensors never change)
+            nonlocal user
+            if "bytes" not in e:
+                if user is None:
+                    user = _tensor_ptrs((self.feat, self.edge_index, self.node_types, self.edge_types))
+                ctx = sum(t.numel() * t.element_size() for t in e["c"].values()
+                          if isinstance(t, torch.Tensor) and t.data_ptr() not in user)
+                e["bytes"] = ctx + (e["plan"].device_bytes() if e["plan"] is not None else 0)
+            return e["bytes"]
         total = {k: nbytes(e) for k, e in self._queries.items()}
         for k in list(self._queries):
             if k == keep:
@@ -345,7 +359,7 @@ class Explainer:
         # multi-GPU: every rank continues from rank 0's generator, so all ranks draw the same
         # masks / sampler seeds / initial weights (checked by checksum below)
         sharding.sync_rng(self.group)
-        self._place_arch(device)
+        params, bufs, mstate = self._place_arch(device)
         clock.mark("prepare")
         # a query explained again (same graph, names, module state) reuses its computational
         # subgraph, plan and arch check: prepare() and the plan build are the run's largest host
@@ -354,61 +368,19 @@ class Explainer:
         entry = self._queries.get(qkey) if qkey is not None else None
         cached = None
         if entry is not None:
-            if _matches(self._query_sources(), entry["src"]) and \
+            if _matches(self._query_sources(params, bufs), entry["src"]) and \
                     self._query_content_ok(element, entry):
                 cached = (entry["c"], entry["plan"], entry["arch_check"])
             else:
                 del self._queries[qkey]  # stale: the inputs changed since it was prepared
         hit = cached is not None
         c = cached[0] if cached else self.prepare(element, device)
-        clock.mark("plan")
         sub_feat, sub_ei, sub_ind, S = c["sub_feat"], c["sub_ei"], c["sub_ind"], c["S"]
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
 
-        if cached:
-            plan, verify = cached[1], None
-        elif self.edge_masks:
-            plan = pipeline.build_edge_plan(self.arch, sub_feat, sub_ei, *c["link"])
-            verify = lambda: pipeline.verify_edge_plan(plan, self.arch, sub_feat, sub_ei, *c["link"])
-        else:
-            plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, [sub_ind], *geo)
-            verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo)
-        clock.mark("verify")
-        arch_check = "off"
-        mode = self.params.get("verify_arch", True)
-        if cached:
-            arch_check = cached[2] if cached[2] in ("off", "failed") else "cached"
-            if mode == "always" and plan is not None:
-                cached = None  # checked again below
-        if plan is not None and mode and not cached:
-            if verify is None:
-                verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo) \
-                    if not self.edge_masks else pipeline.verify_edge_plan(plan, self.arch, sub_feat, sub_ei,
-                                                                          *c["link"])
-            # the check guards the arch lowering (program.compile_arch + the plan's term
-            # dropping), which depends on the module, the graph's type structure and the query
-            # layer's node types: once per module state (parameter storage + in-place version
-            # counters), type structure and lowering per Explainer; params["verify_arch"] =
-            # "always" checks every run
-            key = self._verify_key(plan, c)
-            if mode == "always" or key not in self._verified:
-                ok, err = verify()
-                if not ok:
-                    warnings.warn(f"compiled arch disagrees with its torch forward (max err "
-                                  f"{err:.3g}); using the generic torch path")
-                    plan = None
-                    arch_check = "failed"
-                else:
-                    self._verified.add(key)
-                    arch_check = "verified"
-            else:
-                arch_check = "cached"
-        if qkey is not None:
-            self._queries.pop(qkey, None)  # (re)inserted as the newest entry
-            self._queries[qkey] = {"c": c, "plan": plan, "arch_check": arch_check,
-                                   "src": self._query_sources(),
-                                   "fp": entry["fp"] if hit else self._query_fingerprints()}
-
+        # masks before the plan: the sampler kernels and the initial-weight copy run on the device
+        # while the host builds the plan (the plan build and its arch check draw no numbers from
+        # the global generators, so the reference's RNG order is unchanged)
         clock.mark("sample")
         sampler = self.params.get("mask_sampler", "compat")
         _, epochs = Mask.assertions_mask_generator(self.params)
@@ -458,7 +430,63 @@ class Explainer:
         flat = bits.reshape(times * R, -1)
         g = self.group
         sharding.assert_replicated(bits, "mask rows", g)
-        sharding.assert_replicated(torch.stack(w0_list), "initial surrogate weights", g)
+        w0_all = torch.stack(w0_list)
+        sharding.assert_replicated(w0_all, "initial surrogate weights", g)
+        # the initial weights go to the device now, while the stream holds only the sampler: a
+        # pageable host -> device copy waits for the stream, so issued in the fit phase it held
+        # the host until the forward had finished and left the device idle while the fit launched
+        w0_dev = w0_all.to(device)
+
+        clock.mark("plan")
+
+        if cached:
+            plan, verify = cached[1], None
+        elif self.edge_masks:
+            plan = pipeline.build_edge_plan(self.arch, sub_feat, sub_ei, *c["link"],
+                                            module_state=mstate)
+            verify = lambda: pipeline.verify_edge_plan(plan, self.arch, sub_feat, sub_ei, *c["link"])
+        else:
+            plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, [sub_ind], *geo,
+                                       module_state=mstate)
+            verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo)
+        clock.mark("verify")
+        arch_check = "off"
+        mode = self.params.get("verify_arch", True)
+        if cached:
+            arch_check = cached[2] if cached[2] in ("off", "failed") else "cached"
+            if mode == "always" and plan is not None:
+                cached = None  # checked again below
+        if plan is not None and mode and not cached:
+            if verify is None:
+                verify = lambda: pipeline.verify_plan(plan, self.arch, sub_feat, sub_ei, sub_ind, *geo) \
+                    if not self.edge_masks else pipeline.verify_edge_plan(plan, self.arch, sub_feat, sub_ei,
+                                                                          *c["link"])
+            # the check guards the arch lowering (program.compile_arch + the plan's term
+            # dropping), which depends on the module, the graph's type structure and the query
+            # layer's node types: once per module state (parameter storage + in-place version
+            # counters), type structure and lowering per Explainer; params["verify_arch"] =
+            # "always" checks every run
+            key = self._verify_key(plan, c, mstate)
+            if mode == "always" or key not in self._verified:
+                ok, err = verify()
+                if not ok:
+                    warnings.warn(f"compiled arch disagrees with its torch forward (max err "
+                                  f"{err:.3g}); using the generic torch path")
+                    plan = None
+                    arch_check = "failed"
+                else:
+                    self._verified.add(key)
+                    arch_check = "verified"
+            else:
+                arch_check = "cached"
+        if qkey is not None:
+            self._queries.pop(qkey, None)  # (re)inserted as the newest entry
+            self._queries[qkey] = {"c": c, "plan": plan, "arch_check": arch_check,
+                                   "src": self._query_sources(params, bufs),
+                                   "fp": entry["fp"] if hit else self._query_fingerprints()}
+            if hit and "bytes" in entry and plan is entry["plan"]:
+                self._queries[qkey]["bytes"] = entry["bytes"]
+
         # multi-node-type graphs: the reference's per-copy loop zeroes copies without edges and
         # its extraction re-cuts the [B] outputs (quirk Q4); params["hetero_q4"] = False keeps
         # the per-copy outputs instead (model.py:118-253, wlm.py:435-436)
@@ -511,7 +539,7 @@ class Explainer:
                 fits["best"] = torch.empty(0, dtype=torch.int32, device=device)
                 return torch.empty((0, S), device=device)
             w_, fits["losses"], fits["best"], _, _ = engine.wlm_fit(
-                bits[t0:t1], S, batch, y[t0:t1], kern[t0:t1], torch.stack(w0_list[t0:t1]),
+                bits[t0:t1], S, batch, y[t0:t1], kern[t0:t1], w0_dev[t0:t1],
                 self.params)
             return w_
         w = sharding.gather_map(times, fit, g)
@@ -562,7 +590,7 @@ class Explainer:
             set_seed(self.params["seed"])
         g = self.group
         sharding.sync_rng(g)
-        self._place_arch(device)
+        _, _, mstate = self._place_arch(device)
         c = self.prepare(elements[0], device)
         # graph_prediction: every query indexes the same (whole) graph, so only the element
         # lookup of `prepare` differs per query (explainer.py:427-447)
@@ -574,7 +602,7 @@ class Explainer:
         geo = (c["sub_nt"], c["sub_et"], c["h_ntypes"], c["h_etypes"], c["padded_dims"])
         Q = len(inds)
         assert len(set(inds)) == Q, "run_queries: duplicate query elements"
-        plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, inds, *geo)
+        plan = pipeline.build_plan(self.arch, sub_feat, sub_ei, inds, *geo, module_state=mstate)
         assert plan is not None and not getattr(plan, "multi_type", False), \
             "run_queries needs an engine-compilable single-node-type architecture"
         if self.params.get("verify_arch", True):

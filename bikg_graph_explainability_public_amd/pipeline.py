@@ -35,14 +35,17 @@ def relation_edges(edge_index, edge_type, n_rel):
 _PROGRAMS = collections.OrderedDict()  # compiled_program's cache: key -> (weakref(arch), program)
 
 
-def compiled_program(arch, edge_type_names=None, node_type_names=None):
+def compiled_program(arch, edge_type_names=None, node_type_names=None, state=None):
     """compile_arch(arch, ...) once per module state: keyed by the module (identity, checked by
     weak reference), every parameter and buffer (storage + in-place version counter: an
     optimizer step, load_state_dict or a replaced tensor compiles again) and the type names.
     The program carries the plans' weight-derived device tensors (ForwardPlan._program_tensor),
-    so a new query's plan neither lowers the module nor re-pads its weights.  8 programs kept."""
-    state = tuple((t.data_ptr(), t._version) for t in arch.parameters()) + \
-        tuple((t.data_ptr(), t._version) for t in arch.buffers())
+    so a new query's plan neither lowers the module nor re-pads its weights.  8 programs kept.
+    `state`: the caller's (parameters, buffers) state tuples of this walk (Explainer.run reads
+    them once per call); None reads them here."""
+    if state is None:
+        state = (tuple((t.data_ptr(), t._version) for t in arch.parameters()),
+                 tuple((t.data_ptr(), t._version) for t in arch.buffers()))
     key = (id(arch), state,
            tuple(tuple(e) for e in edge_type_names) if edge_type_names is not None else None,
            tuple(node_type_names) if node_type_names is not None else None)
@@ -58,7 +61,7 @@ def compiled_program(arch, edge_type_names=None, node_type_names=None):
 
 
 def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
-               node_type_names=None, edge_type_names=None, padded_dims=None):
+               node_type_names=None, edge_type_names=None, padded_dims=None, module_state=None):
     """ForwardPlan for `arch` on the (sub)graph, or None when the engine cannot run it.
 
     Multi-node-type graphs (model.py:118-253): the program's terms are gated by destination
@@ -71,7 +74,7 @@ def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
     hetero = edge_type_names is not None and edge_type is not None
     try:
         prog = compiled_program(arch, edge_type_names if hetero else None,
-                                node_type_names if multi else None)
+                                node_type_names if multi else None, module_state)
     except UnsupportedArch as e:
         warnings.warn(f"engine cannot compile arch ({e}); using the generic torch path")
         return None
@@ -100,12 +103,12 @@ def build_plan(arch, feat, edge_index, queries, node_type=None, edge_type=None,
     return plan
 
 
-def build_edge_plan(arch, feat, edge_index, u, v):
+def build_edge_plan(arch, feat, edge_index, u, v, module_state=None):
     """ForwardPlan of an edge problem (edge masks, Data.perturb_edge data.py:500-554): mask
     columns = the subgraph's edges, output = the LinkModel decoder's score of edge (u, v).
     None when the engine cannot compile `arch` (generic torch path)."""
     try:
-        prog = compiled_program(arch)
+        prog = compiled_program(arch, state=module_state)
     except UnsupportedArch as e:
         warnings.warn(f"engine cannot compile arch ({e}); using the generic torch path")
         return None

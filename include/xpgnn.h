@@ -17,6 +17,7 @@
  *   xpg_sample_shapley                 — Mask.shapley_mask           masks.py:231-260
  *   xpg_sample_shapley_dev             — same, device-resident seed (graph replays)
  *   xpg_sample_shapley_sets            — same, one draw per repeat in one call
+ *   xpg_plan_arrays_build / _take      — ForwardPlan receptive-field arrays (host)
  *   xpg_sample_communities             — Mask.get_internal_mask / get_external_indices +
  *                                        Pathways.mask_generator (masks.py:81-194,
  *                                        pathways.py:234-385)
@@ -46,7 +47,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 18
+#define XPG_ABI_VERSION 19
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -104,6 +105,23 @@ int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t
 int xpg_mt19937_community_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t cols,
                                int32_t n_comm, const int32_t* comm_ptr, const int32_t* comm_cols,
                                const int32_t* blocks, int32_t n_blocks, int64_t rows, uint32_t* bits);
+/* HOST functions (no GPU work): the receptive-field plan arrays of a forward plan
+ * (engine.plan_arrays; the frontier walk of Model's L message-passing layers over the
+ * computational subgraph, explainer.py:345-480 / model.py:62-116).  Edges relation by relation
+ * (rel_ptr [n_rel + 1] offsets into src / dst [E]), optional per-edge mask columns eid [E]
+ * (edge-mask plans; NULL = 0), the query positions [nq] (distinct, < S), L layers.  build
+ * computes and keeps the arrays behind *handle and writes their sizes: the L + 1 frontier sizes,
+ * then per CSR (the F_0 degree CSR, then layers 1..L) the sizes of {ptr, src, eid, smul, sptr,
+ * seid}; take copies them back to back into out (int64, the sum of the sizes) and releases the
+ * handle (free releases it without copying).  Frontier L = the queries, frontier l - 1 = frontier
+ * l + its sorted new in-neighbours; CSRs group each target's in-edges (self-loops apart, counted
+ * in smul with their columns in sptr / seid) in edge order, offsets absolute across relations;
+ * the degree CSR holds source node ids, the layer CSRs source positions in F_0 (v19). */
+int xpg_plan_arrays_build(int64_t S, int32_t n_rel, const int64_t* rel_ptr, const int64_t* src,
+                          const int64_t* dst, const int64_t* eid, const int64_t* queries, int64_t nq,
+                          int32_t L, void** handle, int64_t* sizes);
+int xpg_plan_arrays_take(void* handle, int64_t* out);
+int xpg_plan_arrays_free(void* handle);
 /* Same bits, plus counts[r] = popcount of row r (the KernelSHAP coalition sizes, kernels.py:144),
  * accumulated while sampling so KernelSHAP needs no second pass over the bits. */
 int xpg_sample_shapley_counts(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols,

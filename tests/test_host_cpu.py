@@ -459,8 +459,46 @@ def test_take_names_matches_numpy_str_indexing():
     """data.take_names == np.array(names, dtype=str)[idx].tolist() (data.py:341-356) for str,
     int and float names, one index and many."""
     from bikg_graph_explainability_public_amd.data import take_names
-    names = [str(i) for i in range(50)] + [5, 3.5, "x"]
-    for idx in ([1], [0, 5, 49], np.array([50, 51, 52, 3]), torch.tensor([2, 2, 0])):
+    names = [str(i) for i in range(50)] + [5, 3.5, "x", "y\x00", np.str_("z")]
+    for idx in ([1], [0, 5, 49], np.array([50, 51, 52, 3]), torch.tensor([2, 2, 0]), [53, 1],
+                [54, 2]):
         ref = np.array(names, dtype=str)[np.asarray(idx, dtype=np.int64)].tolist()
         assert take_names(names, idx) == ref
     assert take_names(names, []) == []
+
+
+@pytest.mark.parametrize("seed,n_rel,L,nq,with_eid", [(0, 1, 2, 1, False), (1, 3, 2, 4, True),
+                                                      (2, 2, 3, 1, False), (3, 1, 1, 7, True),
+                                                      (4, 5, 2, 2, False)])
+def test_native_plan_arrays_match_numpy(seed, n_rel, L, nq, with_eid):
+    """engine.plan_arrays (the library's host builder, xpg_plan_arrays_build) == the numpy
+    restatement plan_arrays_numpy, array for array: frontiers, degree CSR, every layer's CSRs,
+    self-loop counts and columns, on random multi-relation graphs with self-loops, duplicate
+    edges and isolated nodes."""
+    from bikg_graph_explainability_public_amd.engine import plan_arrays_numpy
+    rng = np.random.default_rng(seed)
+    S = 90
+    rels, eids, col = [], [], 0
+    for r in range(n_rel):
+        E = int(rng.integers(0, 200))
+        ei = rng.integers(0, S - 5, size=(2, E))  # the last 5 nodes stay isolated
+        if E > 6:
+            ei[1, :3] = ei[0, :3]                 # self-loops
+            ei[:, 3:6] = ei[:, :1]                # duplicates of a self-loop
+        rels.append(ei)
+        eids.append(np.arange(col, col + E))
+        col += E
+    q = rng.choice(S, size=nq, replace=False)
+    got = plan_arrays(S, rels, q, L, eids if with_eid else None)
+    ref = plan_arrays_numpy(S, rels, q, L, eids if with_eid else None)
+    for a, b in zip(got["frontiers"], ref["frontiers"]):
+        np.testing.assert_array_equal(a, b)
+    for k in ("deg_ptr", "deg_src", "deg_eid"):
+        np.testing.assert_array_equal(got[k], ref[k])
+    for lg, lr in zip(got["layers"], ref["layers"]):
+        for k in lr:
+            np.testing.assert_array_equal(lg[k], lr[k], err_msg=k)
+    with pytest.raises(ValueError):
+        plan_arrays(S, rels, [S], L)
+    with pytest.raises(ValueError):
+        plan_arrays(S, rels, [1, 1], L)
