@@ -367,7 +367,7 @@ def headline(args, dev, world, rank, workload="c2"):
     split = world > 1 or os.environ.get("XPG_BENCH_SPLIT_GRAPH") == "1"
     # the pipelined graphs need each rank's fits to read only its own rows ((f0, f1) repeats
     # == rows [r0, r1), e.g. times = world): the fit must not regenerate rows from seed_t
-    unroll = 1
+    unroll, depth = 1, 1
     pipe = use_graph and (f0 * R, f1 * R) == (r0, r1) and \
         os.environ.get("XPG_BENCH_PIPE", "1") == "1"
     split = split and not pipe
@@ -472,19 +472,41 @@ def headline(args, dev, world, rank, workload="c2"):
             # A graph holds U consecutive steps (XPG_BENCH_UNROLL, default 4: one launch and one
             # exchange per U steps; U = 1 or even, dividing --steps).  Prologue (untimed): the
             # first repeat's production; the K timed steps do K fits + K productions.
-            W_, nl, nf = (S + 31) // 32, r1 - r0, f1 - f0
-            sets = []
-            for _ in range(2):
-                d = dict(bits=torch.empty((nl, W_), dtype=torch.int32, device=dev),
-                         y=torch.empty((nl, plan.n_out), dtype=torch.float32, device=dev),
-                         k=torch.empty(nl, dtype=torch.float64, device=dev),
-                         cnt=torch.empty(nl, dtype=torch.int32, device=dev),
-                         fit=engine.PreparedFit(nf, R, S, batch, params, dev))
-                statuses.append(d["fit"].status)
-                sets.append(d)
-            s1 = torch.cuda.Stream(device=dev)
+            # Two lanes (default with one rank; XPG_BENCH_FIT_DEPTH=1: one lane): the repeats
+            # alternate between two such pipelines, each with its own buffer sets, side stream
+            # and seed (lane l draws the seeds of steps l, l + 2, ...), whose graphs are replayed
+            # on two streams, so fit i + 1 runs beside fit i (the fits are independent; each is
+            # a latency-bound chain on ~13 workgroups) and a step costs the production rather
+            # than the fit.  (One graph holding both lanes' streams, with event waits between its
+            # side streams, ended in a segfault of hipStreamEndCapture on this stack:
+            # tools/capture_probe.py p2:*.)
             want = max(1, int(os.environ.get("XPG_BENCH_UNROLL", "4")))
-            unroll = next((u for u in range(want, 1, -1) if u % 2 == 0 and args.steps % u == 0), 1)
+
+            def pick_unroll(n):
+                return next((u for u in range(want, 1, -1) if u % 2 == 0 and n % u == 0), 1)
+            n_lanes = 2 if (os.environ.get("XPG_BENCH_FIT_DEPTH", "2") == "2" and world == 1 and
+                            args.steps % 2 == 0) else 1
+            depth = n_lanes
+            per_lane = args.steps // n_lanes
+            unroll = pick_unroll(per_lane)
+            W_, nl, nf = (S + 31) // 32, r1 - r0, f1 - f0
+
+            def make_lane(lane):
+                sets_ = []
+                for _ in range(2):
+                    d = dict(bits=torch.empty((nl, W_), dtype=torch.int32, device=dev),
+                             y=torch.empty((nl, plan.n_out), dtype=torch.float32, device=dev),
+                             k=torch.empty(nl, dtype=torch.float64, device=dev),
+                             cnt=torch.empty(nl, dtype=torch.int32, device=dev),
+                             fit=engine.PreparedFit(nf, R, S, batch, params, dev))
+                    statuses.append(d["fit"].status)
+                    sets_.append(d)
+                seed_l = torch.full((1,), 1000 + args.warmup + lane, dtype=torch.int64, device=dev)
+                return dict(sets=sets_, s1=torch.cuda.Stream(device=dev), ev=torch.cuda.Event(),
+                            seed=seed_l, graphs=[], stream=torch.cuda.Stream(device=dev),
+                            ws=torch.empty(plan.workspace_bytes(nl), dtype=torch.uint8, device=dev))
+            lanes = [make_lane(lane) for lane in range(n_lanes)]
+            sets = lanes[0]["sets"]
             ex = world > 1
             if ex:  # staging row: y fp32 [nl] | k fp64 [nl] | w fp32 [nf, S]
                 oy, ok_ = 0, -(-nl * 4 // 8) * 8
@@ -494,37 +516,36 @@ def headline(args, dev, world, rank, workload="c2"):
                 gath = [torch.zeros((world, unroll, sb), dtype=torch.uint8, device=dev)
                         for _ in range(2)]
 
-            def produce(d):  # (in order on its stream: it is off the fit's critical path)
-                engine.sample_shapley_dev(seed_t, nl, S, row_offset=r0, out=d["bits"])
-                seed_t.add_(1)
-                plan.forward(d["bits"], out=d["y"])
+            def produce(L, d):  # (in order on its stream: it is off the fit's critical path)
+                engine.sample_shapley_dev(L["seed"], nl, S, row_offset=r0, out=d["bits"])
+                L["seed"].add_(n_lanes)
+                plan.forward(d["bits"], out=d["y"], workspace=L["ws"])  # the lane's own workspace
                 engine.shap_kernel(d["bits"], S, out=d["k"], scratch=d["cnt"])
                 d["fit"].prepare(d["bits"], d["y"][:, 0], d["k"], w0[f0:f1])
 
-            prod_ev = torch.cuda.Event()
-
-            def pipe_step(i_set, row):
+            def pipe_step(L, i_set, row):
                 # the fit's Adam steps alone are the chain: the next repeat's production, and
                 # this fit's losses / best epoch / status and its mean / std (or staging copy)
-                # run on s1; the next fit waits only for its production (prod_ev)
+                # run on s1; the next fit waits only for its production (the lane's event)
                 cur = torch.cuda.current_stream()
+                s1 = L["s1"]
                 s1.wait_stream(cur)  # the production rewrites the set the previous fit used
-                d = sets[i_set]
+                d = L["sets"][i_set]
                 w = d["fit"].fit_steps(d["bits"], d["k"])
                 out = None
                 with torch.cuda.stream(s1):
                     if row is not None:  # this step's repeat: logits + kernel weights
                         row[oy:oy + nl * 4].view(torch.float32).copy_(d["y"][:, 0])
                         row[ok_:ok_ + nl * 8].view(torch.float64).copy_(d["k"])
-                    produce(sets[1 - i_set])
-                    prod_ev.record(s1)
+                    produce(L, L["sets"][1 - i_set])
+                    L["ev"].record(s1)
                     s1.wait_stream(cur)  # after this fit's steps
                     d["fit"].finish(d["k"])
                     if row is None:
                         out = part_c(w)
                     else:
                         row[ow:ow + nf * S * 4].view(torch.float32).copy_(w.reshape(-1))
-                cur.wait_event(prod_ev)
+                cur.wait_event(L["ev"])
                 return out
 
             def stacked(b):  # mean / std over all ranks' repeats of replay buffer b's U steps
@@ -533,17 +554,18 @@ def headline(args, dev, world, rank, workload="c2"):
                 std, mean = torch.std_mean(w_all, 1, unbiased=False)
                 return [(mean[j], std[j]) for j in range(unroll)]
 
-            produce(sets[0])  # prologue: the first timed step's repeat
+            for L in lanes:  # prologue: each lane's first timed repeat
+                produce(L, L["sets"][0])
             torch.cuda.synchronize()
-            graphs = []
-            for b in range(2):
-                gph, outs = torch.cuda.CUDAGraph(), []
-                with engine.capture_guard(), torch.cuda.graph(gph):
-                    for j in range(unroll):
-                        outs.append(pipe_step((b * unroll + j) & 1, stage[b][j] if ex else None))
-                    torch.cuda.current_stream().wait_stream(s1)  # join the side stream
-                graphs.append((gph, outs))
-
+            for L in lanes:
+                for b in range(2):
+                    gph, outs = torch.cuda.CUDAGraph(), []
+                    with engine.capture_guard(), torch.cuda.graph(gph):
+                        for j in range(unroll):
+                            outs.append(pipe_step(L, (b * unroll + j) & 1, stage[b][j] if ex else None))
+                        torch.cuda.current_stream().wait_stream(L["s1"])  # join the side stream
+                    L["graphs"].append((gph, outs))
+            graphs = lanes[0]["graphs"]
             def exchange(b):
                 return sharding.all_gather_async(gath[b].view(-1), stage[b].view(-1))
         elif not split:
@@ -571,12 +593,17 @@ def headline(args, dev, world, rank, workload="c2"):
     t0 = time.perf_counter()
     if pipe:
         pending = [None, None]
-        for m in range(args.steps // unroll):
+        for m in range(per_lane // unroll):
             b = m & 1
             if pending[b] is not None:  # replay m - 2's exchange: before its buffer is rewritten
                 pending[b].wait()
                 results += stacked(b)
-            graphs[b][0].replay()
+            if n_lanes == 1:
+                graphs[b][0].replay()
+            else:  # the lanes' graphs on their own streams: the two replays run side by side
+                for L in lanes:
+                    with torch.cuda.stream(L["stream"]):
+                        L["graphs"][b][0].replay()
             if ex:
                 pending[b] = exchange(b)
         for m in range(max(0, args.steps // unroll - 2), args.steps // unroll):
@@ -597,7 +624,8 @@ def headline(args, dev, world, rank, workload="c2"):
     graph_check = exchange_check = None
     if use_graph:  # outside the timed region: the last step == an eager step on the same seed
         if pipe:
-            last = results[-1] if ex else graphs[(args.steps // unroll - 1) & 1][1][-1]
+            # the last step (index K - 1) is the last lane's last step
+            last = results[-1] if ex else lanes[-1]["graphs"][(per_lane // unroll - 1) & 1][1][-1]
         else:
             last = results[-1] if split else g_out
         ref = step(args.warmup + args.steps - 1, False)
@@ -654,6 +682,7 @@ def headline(args, dev, world, rank, workload="c2"):
                                   "sharded by repeat",
                    "mask_sampler": "device (Philox Shapley)",
                    "surrogate_fit": "%s (%d workgroup(s) per fit)" % engine.wlm_plan(f1 - f0, R, S, batch),
+                   "fits_in_flight": depth if pipe else 1,
                    "launch": ("eager" if not use_graph else
                               ("two captured HIP graphs per step (masks -> forward + KernelSHAP; "
                                "surrogate fit) with eager RCCL all-gathers between them"
@@ -661,11 +690,18 @@ def headline(args, dev, world, rank, workload="c2"):
                               f"pipelined captured HIP graphs ({unroll} step(s) per graph "
                               "replay, XPG_BENCH_UNROLL): step i's surrogate "
                               "fit runs beside step i+1's masks -> forward + KernelSHAP "
-                              "(double-buffered; the fit's prologue kernel runs with the "
-                              "production, its losses / best epoch and the mean / std after "
-                              "its Adam steps on the side stream, so consecutive fits' steps "
-                              "run back to back; prologue untimed, K fits + K productions "
-                              "timed)"
+                              + ("and beside fit i+1: the repeats alternate between two such "
+                                 "pipelines (lanes: own buffer sets, side stream and seeds), "
+                                 "whose graphs are replayed on two streams (the fit's prologue "
+                                 "kernel runs with the production, its losses / best epoch and "
+                                 "the mean / std after its Adam steps on the lane's side stream; "
+                                 if depth == 2 else
+                                 "(double-buffered; the fit's prologue kernel runs with the "
+                                 "production, its losses / best epoch and the mean / std after "
+                                 "its Adam steps on the side stream, so consecutive fits' steps "
+                                 "run back to back; ") +
+                              "prologue untimed, K fits + K productions timed; every step is "
+                              "one repeat of its own rows, masks and fit)"
                               if pipe else "one captured HIP graph replayed per step") +
                               " (device-resident sampler seed advanced inside the graph); "
                               "phases_ms from eager steps")},

@@ -1244,8 +1244,18 @@ __device__ uint64_t g_wlm_stamps[2][8];
 // broadcast LDS reads of the layer-1 table row.  Layer-1 outputs are recomputed for each layer-2
 // use instead of stored (a single-query plan uses each once); the layer-2 aggregate stays in
 // registers until the wave-split dense layer and head.
+// Per-XCD count of resident multi-workgroup fit workgroups (k_wlm_fit_mc registers each working
+// workgroup while it holds its CU): the rows forward sizes its per-XCD worker count by it.
+__device__ int g_xcd_busy[16];
+
+__device__ __forceinline__ int xcc_id() { return static_cast<int>(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xFu); }
+
 struct RowsFwdArgs {
   int64_t rows;
+  // XCD-aware block scheduling (nullable): ctl[0] = next 64-row block, ctl[1 + x] = workgroups
+  // started on XCD x (zeroed before the launch); cus_per_xcd = CUs per XCD
+  int* ctl;
+  int cus_per_xcd, n_blocks;
   const uint32_t* bits;
   float* y;
   int words, n0, n_rel, n_layers, out_col, n_last, n_deg_edges, n1_edges, n2_edges;
@@ -1412,19 +1422,36 @@ __device__ __forceinline__ void rows_h1(const RowsFwdArgs& a, const float* lds, 
   }
 }
 
+// Block scheduling.  Without a control block: workgroup b takes 64-row block b.  With one
+// (a.ctl): the dispatcher deals workgroups round-robin over the XCDs, so an XCD that hosts a
+// persistent fit (13 of its 32 CUs held for ~160 us) got as many blocks as the others and ran
+// them in two rounds — the forward took twice as long beside a fit.  Here a workgroup first
+// takes a worker slot on its XCD (at most its free CUs: CUs per XCD minus the fit workgroups
+// registered there) or leaves, and the workers take 64-row blocks from one counter until none is
+// left, so the blocks go where CUs are free.  Every block is taken exactly once either way.
 template <int FS>
 __global__ __launch_bounds__(1024) void k_rows_forward(const RowsFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   int* li = reinterpret_cast<int*>(lds);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t row0 = (int64_t)blockIdx.x * 64, row = row0 + lane;
-  const int nrow = static_cast<int>(a.rows - row0 < 64 ? a.rows - row0 : 64);
+  __shared__ int blk_s;
+  if (a.ctl) {
+    if (tid == 0) {
+      const int x = xcc_id();
+      const int busy = __hip_atomic_load(g_xcd_busy + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int cap = a.cus_per_xcd - busy > 1 ? a.cus_per_xcd - busy : 1;
+      const int slot = __hip_atomic_fetch_add(a.ctl + 1 + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      blk_s = slot < cap ? 0 : -1;
+    }
+    __syncthreads();
+    if (blk_s < 0) return;  // workgroup-uniform: no worker slot left on this XCD
+  }
 #ifdef XPG_WLM_STAMPS
   uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t stamp_last = __builtin_amdgcn_s_memtime();
 #endif
-  {  // LDS image: layer-1 tables, CSR arrays, layer-2 weights, (staged) mask rows
+  {  // LDS image: layer-1 tables, CSR arrays, layer-2 weights
     const int n4 = a.n0 * a.f1_pad / 4;
     for (int k = 0; k < a.n_terms1; ++k) {
       const float4* src = reinterpret_cast<const float4*>(a.tab1[k]);
@@ -1460,12 +1487,26 @@ __global__ __launch_bounds__(1024) void k_rows_forward(const RowsFwdArgs a) {
       for (int e = tid; e < n; e += 1024)
         reinterpret_cast<float4*>(lds + a.o_hw[i])[e] = reinterpret_cast<const float4*>(a.H[i].weight)[e];
     }
-    if (a.stage_bits) {
-      uint32_t* mb = reinterpret_cast<uint32_t*>(lds + a.o_mb);
-      for (int e = tid; e < 64 * a.words; e += 1024) {
-        const int r = e / a.words, w = e - r * a.words;
-        mb[r * a.mb_pitch + w] = r < nrow ? a.bits[(row0 + r) * a.words + w] : 0u;
-      }
+  }
+  for (int it = 0;; ++it) {
+  int64_t blk;
+  if (a.ctl) {
+    __syncthreads();  // blk_s of the previous block read by every thread
+    if (tid == 0) blk_s = __hip_atomic_fetch_add(a.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    blk = blk_s;
+    if (blk >= a.n_blocks) break;
+  } else {
+    if (it > 0) break;
+    blk = blockIdx.x;
+  }
+  const int64_t row0 = blk * 64, row = row0 + lane;
+  const int nrow = static_cast<int>(a.rows - row0 < 64 ? a.rows - row0 : 64);
+  if (a.stage_bits) {  // this block's mask rows
+    uint32_t* mbw = reinterpret_cast<uint32_t*>(lds + a.o_mb);
+    for (int e = tid; e < 64 * a.words; e += 1024) {
+      const int r = e / a.words, w = e - r * a.words;
+      mbw[r * a.mb_pitch + w] = r < nrow ? a.bits[(row0 + r) * a.words + w] : 0u;
     }
   }
   __syncthreads();
@@ -1654,6 +1695,7 @@ __global__ __launch_bounds__(1024) void k_rows_forward(const RowsFwdArgs a) {
     __syncthreads();
     XPG_STAMP(6)
   }
+  }  // blocks
 #ifdef XPG_WLM_STAMPS
   if (blockIdx.x == 0 && (tid == 0 || tid == 1023)) {
     for (int q = 0; q < 8; ++q) g_wlm_stamps[tid == 0 ? 0 : 1][q] = stamp_acc[q];
@@ -4076,6 +4118,9 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
     f = blockIdx.x / P;
     part = static_cast<int>(blockIdx.x - f * P);
   }
+  // this workgroup holds its CU until the fit ends: counted on its XCD (k_rows_forward)
+  const int my_xcc = xcc_id();
+  if (tid == 0) __hip_atomic_fetch_add(g_xcd_busy + my_xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int64_t nsteps = (rows + batch - 1) / batch;
   const int w_lo = min(words, part * wpp), w_hi = min(words, w_lo + wpp);
   const int ow = w_hi - w_lo;                       // own words (>= 1: P = ceil(words / wpp))
@@ -4386,6 +4431,7 @@ __global__ __launch_bounds__(1024) void k_wlm_fit_mc(
       vg[i] = v[c];
     }
   }
+  if (tid == 0) __hip_atomic_fetch_add(g_xcd_busy + my_xcc, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #undef XPG_MC_LOAD
 #undef XPG_MC_STORE
 }
@@ -4760,7 +4806,7 @@ int deg_pitch(const xpg_forward_plan* p) {
 }
 
 struct WsLayout {
-  size_t kin = 0, agg = 0, head0 = 0, head1 = 0, total = 0;
+  size_t kin = 0, agg = 0, head0 = 0, head1 = 0, ctl = 0, total = 0;
   size_t h[64];
 };
 
@@ -4791,6 +4837,8 @@ int layout_ws(const xpg_forward_plan* p, int64_t rows, WsLayout* L) {
   off += align_up(hmax);
   L->head1 = off;
   off += align_up(hmax);
+  L->ctl = off;  // the rows forward's block-scheduling counters (zeroed before each launch)
+  off += align_up(sizeof(int) * 32);
   L->total = off;
   return XPG_OK;
 }
@@ -5341,7 +5389,8 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
 }
 
 // Lanes-=-rows fused forward for 1- and 2-layer plans (returns 1 when it does not apply).
-int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st) {
+int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t rows, float* y, hipStream_t st,
+                     int* ctl) {
   if (p->n_layers < 1 || p->n_layers > 2 || p->n_head > kFusedMaxHead || plan_multi_type(p)) return 1;
   if (p->edge_masks || p->edge_dot) return 1;  // edge problems: multi-kernel path only
   RowsFwdArgs a;
@@ -5465,7 +5514,15 @@ int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t ro
     if (off + n <= cap) a.o_hw[i] = take(n);
   }
   const size_t lds = sizeof(float) * (size_t)off;
-  const dim3 grid(static_cast<unsigned>(cdiv(rows, 64)));
+  a.n_blocks = static_cast<int>(cdiv(rows, 64));
+  a.cus_per_xcd = std::max(1, device_cus() / 8);
+  a.ctl = ctl;
+  unsigned nwg = static_cast<unsigned>(a.n_blocks);
+  if (ctl) {  // one workgroup per CU at most (LDS-bound); extra ones leave at once
+    XPG_HIP(hipMemsetAsync(ctl, 0, sizeof(int) * 32, st));
+    nwg = static_cast<unsigned>(std::min<int64_t>(8 * a.cus_per_xcd, (int64_t)a.n_blocks + 4 * a.cus_per_xcd));
+  }
+  const dim3 grid(nwg);
 #define XPG_ROWS(F)                                                                                     \
   if (fs == F) {                                                                                        \
     XPG_HIP(lds_limit(reinterpret_cast<const void*>(&k_rows_forward<F>)));      \
@@ -5856,7 +5913,7 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
       rc = try_fused_forward(p, bits, rows, y, st);
       if (rc != 1) return rc;
     } else if (!multi) {
-      rc = try_rows_forward(p, bits, rows, y, st);
+      rc = try_rows_forward(p, bits, rows, y, st, reinterpret_cast<int*>(static_cast<char*>(workspace) + L.ctl));
       if (rc != 1) return rc;
     }
     if (strict) return fail(XPG_EINVAL, "masked_forward: the forced XPG_FORWARD path does not take this plan");

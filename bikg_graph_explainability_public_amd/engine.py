@@ -748,10 +748,14 @@ class ForwardPlan:
         _lib.check(_lib.load().xpg_forward_workspace(ctypes.byref(self.desc), rows, ctypes.byref(n)))
         return n.value
 
-    def forward(self, bits: torch.Tensor, max_ws_bytes=8 << 30, out: torch.Tensor = None) -> torch.Tensor:
+    def forward(self, bits: torch.Tensor, max_ws_bytes=8 << 30, out: torch.Tensor = None,
+                workspace: torch.Tensor = None) -> torch.Tensor:
         """y [rows, n_out] fp32: model output at each target of the last conv layer, per mask
         row (wlm.py:349-436 for one batch, all batches at once).  `out`: a contiguous fp32
-        [rows, n_out] tensor to write y into (no allocation once the workspace exists)."""
+        [rows, n_out] tensor to write y into (no allocation once the workspace exists).
+        `workspace`: a uint8 device tensor of at least workspace_bytes(rows) to use instead of the
+        plan's own — forwards running at the same time on different streams need one each (the
+        workspace holds the launch's block-scheduling counters)."""
         _lib.require_device(bits, "bits")
         rows = bits.shape[0]
         if out is None:
@@ -763,6 +767,14 @@ class ForwardPlan:
             y = out
         if rows == 0:
             return y
+        st = _lib.stream_of(self.device)
+        if workspace is not None:
+            if workspace.dtype != torch.uint8 or workspace.device != self.device or \
+                    workspace.numel() < self.workspace_bytes(rows):
+                raise ValueError("workspace must be a uint8 device tensor of workspace_bytes(rows)")
+            call("xpg_masked_forward", ctypes.byref(self.desc), ptr(bits), rows, ptr(y),
+                 ptr(workspace), workspace.numel(), st)
+            return y
         w1, w2 = self.workspace_bytes(1), self.workspace_bytes(2)
         per_row = max(0, w2 - w1)  # 0: a rows-independent workspace (the wide 32-row passes)
         fixed = max(0, w1 - per_row)
@@ -771,7 +783,6 @@ class ForwardPlan:
         need = self.workspace_bytes(chunk)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        st = _lib.stream_of(self.device)
         for r0 in range(0, rows, chunk):
             n = min(chunk, rows - r0)
             call("xpg_masked_forward", ctypes.byref(self.desc), ptr(bits[r0:r0 + n]), n,

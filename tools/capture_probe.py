@@ -14,6 +14,16 @@ one line per variant and stops at the first child killed by a signal:
   ext_wait    a side stream waits on an event recorded BEFORE the capture, then joins
   replay_in   another graph replayed while this one is being captured
   graph_gc    a graph object dropped (freed) while another is being captured
+  multi_side  four side streams forked from the capture stream, work on each, all joined
+  xstream_ev  side stream A records an event after its work, side stream B waits for it, then
+              works; both joined
+  ev_rerecord one event recorded twice on A (after two pieces of work), waited by B after the
+              first record and by C after the second; all joined
+  ev_dangling an event recorded on a joined side stream that nothing waits for
+  pipe2       bench.py's fit-depth-2 pipelined topology with torch ops standing in for the
+              kernels: two graphs of 4 steps, 4 buffer sets, two fit streams, a production and a
+              finish stream, per-set events waited only inside their own capture
+  pipe2_fresh pipe2 with new event objects for each capture (no event recorded in two captures)
 
     python tools/capture_probe.py [variant ...]
 """
@@ -21,11 +31,82 @@ import subprocess
 import sys
 
 VARIANTS = ("joined", "sync", "alloc_side", "unjoined", "timing_ev", "ext_wait", "replay_in",
-            "graph_gc")
+            "graph_gc", "multi_side", "xstream_ev", "ev_rerecord", "ev_dangling", "pipe2_fresh", "pipe2")
+
+
+def pipe2(fresh=False, graphs_n=2, ev_prod=True, ev_fin=True, ev_fit=True, unroll=4):
+    import torch
+    dev = torch.device("cuda", 0)
+    n_sets = 4
+    sets = [torch.zeros(1 << 16, device=dev) for _ in range(n_sets)]
+    res = [torch.zeros(1 << 16, device=dev) for _ in range(n_sets)]
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    fs = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    prod = [torch.cuda.Event() for _ in range(n_sets)]
+    fit = [torch.cuda.Event() for _ in range(n_sets)]
+    fin = [torch.cuda.Event() for _ in range(n_sets)]
+    sets[0].fill_(1.0)
+    torch.cuda.synchronize()
+    graphs = []
+    for b in range(graphs_n):
+        g = torch.cuda.CUDAGraph()
+        if fresh:  # event objects of this capture only (none re-recorded in another capture)
+            prod = [torch.cuda.Event() for _ in range(n_sets)]
+            fit = [torch.cuda.Event() for _ in range(n_sets)]
+            fin = [torch.cuda.Event() for _ in range(n_sets)]
+        with torch.cuda.graph(g):
+            cur = torch.cuda.current_stream()
+            for st in (s1, s2, *fs):
+                st.wait_stream(cur)
+            rec = set()
+            for j in range(unroll):
+                i = b * unroll + j
+                a, nb = i % n_sets, (i + 1) % n_sets
+                f = fs[i & 1]
+                if ("prod", a) in rec:
+                    f.wait_event(prod[a])
+                elif not ev_prod and j > 0:
+                    f.wait_stream(s1)
+                with torch.cuda.stream(f):
+                    res[a].copy_(sets[a] * 2.0)
+                    if ev_fit:
+                        fit[a].record(f)
+                with torch.cuda.stream(s1):
+                    if ("fin", nb) in rec:
+                        s1.wait_event(fin[nb])
+                    elif not ev_fin:
+                        s1.wait_stream(s2)
+                    sets[nb].fill_(float(i + 2))
+                    if ev_prod and j + 1 < unroll:
+                        prod[nb].record(s1)
+                        rec.add(("prod", nb))
+                if ev_fit:
+                    s2.wait_event(fit[a])
+                else:
+                    s2.wait_stream(f)
+                with torch.cuda.stream(s2):
+                    res[a].add_(0.5)
+                    if ev_fin and j + n_sets - 1 < unroll:
+                        fin[a].record(s2)
+                        rec.add(("fin", a))
+            for st in (s1, s2, *fs):
+                cur.wait_stream(st)
+        graphs.append(g)
+    for m in range(4):
+        graphs[m % graphs_n].replay()
+    torch.cuda.synchronize()
+    print(f"pipe2 (fresh={fresh} graphs={graphs_n} ev prod/fin/fit={ev_prod}/{ev_fin}/{ev_fit} u={unroll}): capture + replay ok, res[3][0] = {float(res[3][0])}", flush=True)
 
 
 def child(variant):
     import torch
+    if variant in ("pipe2", "pipe2_fresh"):
+        return pipe2(fresh=variant == "pipe2_fresh")
+    if variant.startswith("p2:"):  # p2:g=1,prod=0,fin=1,fit=1,u=4
+        kv = dict(x.split("=") for x in variant[3:].split(","))
+        return pipe2(graphs_n=int(kv.get("g", 2)), ev_prod=kv.get("prod", "1") == "1",
+                     ev_fin=kv.get("fin", "1") == "1", ev_fit=kv.get("fit", "1") == "1",
+                     unroll=int(kv.get("u", 4)))
     dev = torch.device("cuda", 0)
     x = torch.ones(1 << 20, device=dev)
     side = torch.cuda.Stream(device=dev)
@@ -54,6 +135,41 @@ def child(variant):
             del other
             import gc
             gc.collect()
+        elif variant in ("multi_side", "xstream_ev", "ev_rerecord", "ev_dangling"):
+            ss = [torch.cuda.Stream(device=dev) for _ in range(4)]
+            for st in ss:
+                st.wait_stream(cur)
+            ev = torch.cuda.Event()
+            if variant == "multi_side":
+                for k, st in enumerate(ss):
+                    with torch.cuda.stream(st):
+                        y[k::4].add_(1.0)
+            elif variant == "xstream_ev":
+                with torch.cuda.stream(ss[0]):
+                    y.add_(1.0)
+                    ev.record(ss[0])
+                ss[1].wait_event(ev)
+                with torch.cuda.stream(ss[1]):
+                    y.mul_(2.0)
+            elif variant == "ev_rerecord":
+                with torch.cuda.stream(ss[0]):
+                    y.add_(1.0)
+                    ev.record(ss[0])
+                ss[1].wait_event(ev)
+                with torch.cuda.stream(ss[1]):
+                    x.add_(0.0)
+                with torch.cuda.stream(ss[0]):
+                    y.add_(1.0)
+                    ev.record(ss[0])
+                ss[2].wait_event(ev)
+                with torch.cuda.stream(ss[2]):
+                    y.mul_(1.0)
+            else:
+                with torch.cuda.stream(ss[0]):
+                    y.add_(1.0)
+                    ev.record(ss[0])
+            for st in ss:
+                cur.wait_stream(st)
         elif variant == "sync":
             float(y.sum().item())
         elif variant == "alloc_side":
