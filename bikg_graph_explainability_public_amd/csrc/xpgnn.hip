@@ -1393,20 +1393,23 @@ __device__ __forceinline__ void rows_h1(const RowsFwdArgs& a, const float* lds, 
     // GCN edge factor dv_u * dt; MEAN: [u kept] / cnt = min(dv_u * BIG, 1) * inv (dv > 0 iff kept)
     const float gmul = kind == XPG_TERM_GCN ? cedge_t : 0.f;
     const float mmul = kind == XPG_TERM_GCN ? 0.f : cedge_t;
+    // in-edges per batch (their LDS reads in flight together); 8 and 16 measured slower at c2
+    // (59.8 -> 62.1 / 64.5 us per forward), equal at c3node: profiles/r5_rows_edge_batch_ab.log
+    constexpr int EB = 4;
     for (int wb = e0; wb < e1; wb += 64) {
       const int ne = min(64, e1 - wb);
       const int vsrc = li[a.o_l1f0 + wb + min(lane, ne - 1)];
-      for (int i0 = 0; i0 < ne; i0 += 4) {
-        int u[4];
-        float d[4], v[4][FS];
+      for (int i0 = 0; i0 < ne; i0 += EB) {
+        int u[EB];
+        float d[EB], v[EB][FS];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) u[q] = rdl(vsrc, min(i0 + q, ne - 1));
+        for (int q = 0; q < EB; ++q) u[q] = rdl(vsrc, min(i0 + q, ne - 1));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) d[q] = dvr[u[q] * 64];
+        for (int q = 0; q < EB; ++q) d[q] = dvr[u[q] * 64];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ld_fs<FS>(T + u[q] * a.f1_pad, v[q]);
+        for (int q = 0; q < EB; ++q) ld_fs<FS>(T + u[q] * a.f1_pad, v[q]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < EB; ++q) {
           const float valid = static_cast<float>(i0 + q < ne);
           const float c = valid * fmaf(d[q], gmul, fminf(d[q] * 1e30f, 1.f) * mmul);
 #pragma unroll
