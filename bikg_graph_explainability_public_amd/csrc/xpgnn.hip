@@ -4524,8 +4524,8 @@ __global__ __launch_bounds__(256) void k_wlm_loss_best(const float* __restrict__
 //              (5 butterfly stages), then one lookup per nibble into 4-row tables of g; the four
 //              waves' column sums meet in LDS; Adam update of the chunk's columns and sum |w|
 constexpr int kGwWords = 64;    // mask words per chunk (2048 columns)
-constexpr int kGpWaves = 8;     // k_gw_p: waves per workgroup
-constexpr int kGgWaves = 4;     // k_gw_grad: waves per workgroup
+constexpr int kGpWaves = 8;     // k_gw_p: waves per workgroup (16: slower, r5_grid_fit_waves_ab.log)
+constexpr int kGgWaves = 4;     // k_gw_grad: waves per workgroup (8: slower)
 
 // Sum of v[0..31] over the wave's 64 lanes for every i: after the call lanes 2i and 2i + 1 hold
 // sum_lanes v[i] in v[0] (5 halving exchange stages + a final pair add).
