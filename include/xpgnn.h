@@ -252,7 +252,9 @@ typedef struct xpg_forward_plan {
 int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* bytes);
 /* y[r * n_last + i] = model output (column out_col) of target i of the last conv layer for
  * mask row r (n_last = layers[n_layers-1].n_tgt; 1 for a single query); with edge_dot set,
- * y[r] = the decoded score of the target pair (dot_a, dot_b). */
+ * y[r] = the decoded score of the target pair (dot_a, dot_b).  The workspace also holds the
+ * launch's block-scheduling counters (zeroed on the stream before the kernel): calls that may
+ * run at the same time (different streams) need workspaces of their own. */
 int xpg_masked_forward(const xpg_forward_plan* plan, const uint32_t* bits, int64_t rows,
                        float* y, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
 

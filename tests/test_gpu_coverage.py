@@ -731,3 +731,51 @@ def test_explainer_arch_check_keyed_on_query_lowering():
         dff, _ = fresh.run(q, 1)
         assert fresh.last_run["arch_check"] == "verified"
         assert df.equals(dff)
+
+
+def test_rows_forward_concurrent_with_fits_and_forwards():
+    """The rows forward's XCD-aware block scheduling (k_rows_forward takes worker slots on each
+    XCD sized by the fit workgroups registered there, then 64-row blocks from one counter): two
+    forwards on two streams with workspaces of their own, launched while two multi-workgroup
+    fits run on two more streams, give the outputs of a forward run alone bit for bit, and the
+    fits are unchanged too."""
+    import argparse
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    e = _eng()
+    args = argparse.Namespace(nodes=100_000, edges=1_000_000, feat=64, query=7)
+    _, _, _, _, plan = bench.build_c2(args, DEV)
+    S, R, batch = plan.cols, 12800, 256
+    bits = [e.sample_shapley(11 + i, R, S, DEV) for i in range(2)]
+    ref = [plan.forward(b).clone() for b in bits]
+    ys = [plan.forward(b)[:, 0].contiguous() for b in bits]
+    ks = [e.shap_kernel(b, S) for b in bits]
+    w0 = torch.zeros((1, S), device=DEV)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    fits = [e.PreparedFit(1, R, S, batch, params, DEV) for _ in range(2)]
+    for f, b, y, k in zip(fits, bits, ys, ks):
+        f.prepare(b, y, k, w0)
+    w_alone = []
+    for f, b, k in zip(fits, bits, ks):
+        w_alone.append(f.fit(b, k).clone())
+        f.prepare(b, ys[fits.index(f)], k, w0)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=DEV) for _ in range(4)]
+    wss = [torch.empty(plan.workspace_bytes(R), dtype=torch.uint8, device=DEV) for _ in range(2)]
+    outs = [torch.empty_like(r) for r in ref]
+    w_conc = [None, None]
+    for rep in range(3):
+        for j in range(2):  # the fits first: their workgroups hold CUs while the forwards start
+            with torch.cuda.stream(streams[j]):
+                w_conc[j] = fits[j].fit(bits[j], ks[j])
+        for j in range(2):
+            with torch.cuda.stream(streams[2 + j]):
+                plan.forward(bits[j], out=outs[j], workspace=wss[j])
+        torch.cuda.synchronize()
+        for j in range(2):
+            assert torch.equal(outs[j], ref[j]), (rep, j)
+            assert torch.equal(w_conc[j], w_alone[j]), (rep, j)
+            fits[j].prepare(bits[j], ys[j], ks[j], w0)
+        torch.cuda.synchronize()
+    for f in fits:
+        e.check_fit_status(f.status)
