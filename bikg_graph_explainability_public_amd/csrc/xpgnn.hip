@@ -870,21 +870,25 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
   }
 }
 
-// Layer-1 aggregation with lanes = mask rows (W = 32 or 64 features, no edge masks): wave = (block
-// of 64 mask rows, one target).  The tables are shared by every mask row, so each in-edge's table
-// row is a wave-uniform read (scalar loads) added to the lanes that keep the edge; only the
-// per-row keep bits / degrees are per-lane loads.  k_agg<true> instead gives each (row, target)
-// item 16 lanes that fetch every kept row's table slice themselves: for small frontiers and many
-// rows (the c5 shape) that re-reads the same few KB of table per mask row.  Same operations per
+// Layer-1 aggregation with lanes = mask rows (no edge masks): wave = (block of 64 mask rows, one
+// target, one W-feature slice of the layer's a.width = W, 2W, 4W features).  The tables are shared
+// by every mask row, so each in-edge's table slice is a wave-uniform read (scalar loads) added to
+// the lanes that keep the edge; only the per-row keep bits / degrees are per-lane loads.
+// k_agg<true> instead gives each (row, target) item 16-32 lanes that fetch every kept row's table
+// slice themselves: for small frontiers and many rows (the c5 shape; c3 node_prediction's 128-wide
+// SAGE tables) that re-reads the same table rows from L2 once per mask row.  Same operations per
 // value in the same order as k_agg<true> (bitwise the same h1).
 template <int W>
 __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
   const int64_t wid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int64_t nblk = (a.rows + 63) / 64;
-  if (wid >= nblk * a.n_tgt) return;  // wave-uniform
-  const int t = static_cast<int>(wid % a.n_tgt);
-  const int64_t b0 = (wid / a.n_tgt) * 64, b = b0 + lane;
+  const int nsl = a.width / W;  // feature slices (host-checked: a.width = nsl * W)
+  if (wid >= nblk * a.n_tgt * nsl) return;  // wave-uniform
+  const int fo = static_cast<int>(wid % nsl) * W;
+  const int64_t wt = wid / nsl;
+  const int t = static_cast<int>(wt % a.n_tgt);
+  const int64_t b0 = (wt / a.n_tgt) * 64, b = b0 + lane;
   const bool vrow = b < a.rows;
   const int64_t bb = vrow ? b : b0;
   const float* kb = a.kin + bb * (int64_t)a.n_rel * a.kpitch;
@@ -897,8 +901,8 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
     const int kind = a.kind[k];
     const int r = a.rel[k];
     if (a.tgt_type && a.dst_type[k] >= 0 && a.tgt_type[t] != a.dst_type[k]) continue;  // uniform
-    const float* __restrict__ T = a.table[k];
-    const float* __restrict__ selfrow = T + (int64_t)t0 * W;
+    const float* __restrict__ T = a.table[k] + fo;
+    const float* __restrict__ selfrow = T + (int64_t)t0 * a.width;
     float s[W];
     if (kind == XPG_TERM_ROOT) {
 #pragma unroll
@@ -919,7 +923,7 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
           const float ku = kb[(int64_t)r * a.kpitch + u0];
           if (kt >= 0.f && ku >= 0.f) {
             const float c = inv_sqrt_deg(ku) * dt;
-            const float* __restrict__ src = T + (int64_t)u0 * W;
+            const float* __restrict__ src = T + (int64_t)u0 * a.width;
 #pragma unroll
             for (int f = 0; f < W; ++f) s[f] = fmaf(c, src[f], s[f]);
           }
@@ -935,7 +939,7 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
           const int u0 = a.agg_f0[e];
           const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
           if (keep) {
-            const float* __restrict__ src = (a.rows_blk & 2) ? selfrow : T + (int64_t)u0 * W;
+            const float* __restrict__ src = (a.rows_blk & 2) ? selfrow : T + (int64_t)u0 * a.width;
 #pragma unroll
             for (int f = 0; f < W; ++f) s[f] += src[f];
           }
@@ -954,9 +958,9 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
   // in 32-float column chunks, so every store instruction writes whole 128-B lines (8 rows x
   // 128 B).  Stored straight from the lanes (each lane its own 256-B row, 16 B per instruction,
   // 64 lines per instruction), the lines sat half-written in L2 and HBM saw ~2.4x the bytes.
-  const float* bias = a.bias + (a.tgt_type ? (int64_t)a.tgt_type[t] * a.width : 0);
+  const float* bias = a.bias + (a.tgt_type ? (int64_t)a.tgt_type[t] * a.width : 0) + fo;
 #pragma unroll
-  for (int f = 0; f < W; ++f) tot[f] = (f < a.f_real) ? act_apply(tot[f] + bias[f], a.act) : 0.f;
+  for (int f = 0; f < W; ++f) tot[f] = (fo + f < a.f_real) ? act_apply(tot[f] + bias[f], a.act) : 0.f;
   __shared__ float l1o[4][64 * 33];
   float* tile = l1o[threadIdx.x >> 6];
   const int rr = lane >> 3, q = lane & 7;  // store phase: row rr + 8 i, float4 q of the chunk
@@ -971,7 +975,7 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
       const float* src = tile + row * 33 + 4 * q;
       const float4 v = make_float4(src[0], src[1], src[2], src[3]);
       if (b0 + row < a.rows)
-        *reinterpret_cast<float4*>(a.out + ((b0 + row) * a.n_tgt + t) * a.out_ld + 32 * c + 4 * q) = v;
+        *reinterpret_cast<float4*>(a.out + ((b0 + row) * a.n_tgt + t) * a.out_ld + fo + 32 * c + 4 * q) = v;
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -4872,17 +4876,18 @@ int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t
 template <bool L1>
 int launch_agg(const AggArgs& a, hipStream_t st) {
   XPG_REQ(a.width % 32 == 0 && a.width > 0, "agg: row width must be a positive multiple of 32");
-  // layer 1, widths 32 / 64, no edge masks: lanes = mask rows (XPG_AGG_GENERIC=1, a diagnostics
+  // layer 1, widths 32 / 64 / 128 / 256, no edge masks: lanes = mask rows (XPG_AGG_GENERIC=1, a diagnostics
   // switch: the generic k_agg, which the parity suite compares bitwise)
   int generic = 0;
   if (const int rc = diag_env("XPG_AGG_GENERIC", &generic)) return rc;
-  if (L1 && !a.agg_eid && (a.width == 32 || a.width == 64) && !generic) {
-    const int64_t waves = cdiv(a.rows, 64) * a.n_tgt;
+  if (L1 && !a.agg_eid && (a.width == 32 || a.width == 64 || a.width == 128 || a.width == 256) && !generic) {
+    const int slice = a.width == 32 ? 32 : 64;  // features per wave
+    const int64_t waves = cdiv(a.rows, 64) * a.n_tgt * (a.width / slice);
     if (waves == 0) return XPG_OK;
     const dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
     AggArgs b = a;
     if (const int rc = diag_env("XPG_L1_DBG", &b.rows_blk)) return rc;
-    if (a.width == 64) hipLaunchKernelGGL(k_agg_l1_rows<64>, grid, block, 0, st, b);
+    if (slice == 64) hipLaunchKernelGGL(k_agg_l1_rows<64>, grid, block, 0, st, b);
     else hipLaunchKernelGGL(k_agg_l1_rows<32>, grid, block, 0, st, b);
     XPG_LAUNCHED();
     return XPG_OK;
