@@ -624,10 +624,12 @@ __global__ void k_shap_clean(int64_t rows, double* __restrict__ out) {
 }
 
 // ------------------------------------------------------------------------------------ dense
-// C = act(A W^T + b) on v_mfma_f32_32x32x2_f32.  One wave owns 32 rows x (NT*32) columns; the
-// k loop advances 8 at a time: each lane loads one float4 of its A row and one float4 of each
-// W row, feeding 4 MFMAs whose 2 k-slots map to k = kc + 4*h + s (h = lane >> 5), identically
-// for A and B, so the contraction is exact.  C/D map: col = lane & 31,
+// C = act(A W^T + b) on v_mfma_f32_32x32x2_f32.  One wave owns 32 rows x (NT*32) columns
+// (column group cg of n_groups: consecutive waves take the column groups of one 32-row block, so
+// a workgroup's waves share its A rows in L1 and a wide layer spreads over n_groups x as many
+// waves); the k loop advances 8 at a time: each lane loads one float4 of its A row and one
+// float4 of each W row, feeding 4 MFMAs whose 2 k-slots map to k = kc + 4*h + s (h = lane >> 5),
+// identically for A and B, so the contraction is exact.  C/D map: col = lane & 31,
 // row = (reg & 3) + 8 * (reg >> 2) + 4 * h.
 template <int NT>
 __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int64_t M, int64_t lda,
@@ -635,10 +637,17 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
                                                const float* __restrict__ bias, int n_real, int act,
                                                float* __restrict__ C, int64_t ldc,
                                                const int32_t* __restrict__ row_type, int64_t type_mod,
-                                               int bias_ld) {
+                                               int bias_ld, int n_groups) {
   const int lane = threadIdx.x & 63;
-  const int64_t m0 = (blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 32;
+  const int64_t wv = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int cg = static_cast<int>(wv % n_groups);
+  const int64_t m0 = (wv / n_groups) * 32;
   if (m0 >= M) return;
+  const int c0 = cg * NT * 32;  // first column of this wave's group
+  W += (int64_t)c0 * ldw;
+  bias += c0;
+  C += c0;
+  n_real -= c0;
   const int i = lane & 31, h = lane >> 5;
   const int64_t arow = m0 + i;
   const bool a_ok = arow < M;
@@ -667,7 +676,8 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
     for (int reg = 0; reg < 16; ++reg) {
       const int64_t m = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
       // multi-node-type layers: the bias of the row's target type (rows are (mask row, target))
-      const float b = (row_type && m < M && col < n_real) ? bias[(int64_t)row_type[m % type_mod] * bias_ld + col] : bv;
+      const float b = (row_type && m < M && col < n_real) ? bias[(int64_t)row_type[m % type_mod] * bias_ld + col]
+                                                          : bv;
       if (m < M) C[m * ldc + col] = col < n_real ? act_apply(acc[nt][reg] + b, act) : 0.f;
     }
   }
@@ -4857,13 +4867,17 @@ int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t
           "xpg_dense: k_pad % 8, n_pad in {32..256} step 32 required");
   XPG_REQ(lda % 4 == 0 && ldw % 4 == 0, "xpg_dense: lda/ldw must be multiples of 4");
   if (M <= 0) return XPG_OK;
-  const int64_t waves = cdiv(M, 32);
+  // 4+ column tiles: split them over column groups of one or two tiles per wave (a 128-wide layer
+  // on one wave per 32 rows left a workgroup of 4 waves per CU, latency-bound)
+  const int tiles = static_cast<int>(n_pad / 32);
+  const int groups = tiles >= 4 && tiles % 4 == 0 ? 4 : 1;
+  const int64_t waves = cdiv(M, 32) * groups;
   dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
   const int kp = static_cast<int>(k_pad), nr = static_cast<int>(n_real);
-  switch (n_pad / 32) {
+  switch (tiles / groups) {
 #define XPG_DENSE_CASE(NT) \
     case NT: hipLaunchKernelGGL(k_dense<NT>, grid, block, 0, st, A, M, lda, W, ldw, kp, bias, nr, act, C, ldc, \
-                                row_type, type_mod, bias_ld); break;
+                                row_type, type_mod, bias_ld, groups); break;
     XPG_DENSE_CASE(1) XPG_DENSE_CASE(2) XPG_DENSE_CASE(3) XPG_DENSE_CASE(4)
     XPG_DENSE_CASE(5) XPG_DENSE_CASE(6) XPG_DENSE_CASE(7) XPG_DENSE_CASE(8)
 #undef XPG_DENSE_CASE
