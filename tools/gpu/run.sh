@@ -59,6 +59,11 @@ for step in "$@"; do
            run pmc_fetch_c3 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 && \
            run pmc_write_c3 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 ;;
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
+    # k_agg_l1_rows ablations on the rows_ab plans (XPG_L1_DBG 1: no keep loads, 2: every source
+    # the self row, 3: both; outputs invalid) + the kernel stats of the unablated run
+    l1abl) for d in 0 1 2 3; do XPG_DIAGNOSTICS=1 XPG_L1_DBG=$d run l1abl_$d 200 python -u tools/rows_ab.py || exit 1; done && \
+           cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run rowsprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rowsprof -o run -- python3 tools/rows_ab.py ;;
     apiprof3) run apiprof3 300 python -u tools/api_profile.py --graph c3 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
               run apitrace3 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/apitrace3 -o run -- python3 tools/api_profile.py --graph c3 --top 5 ;;
     widetests) run widetests 600 python -u -m pytest tests/test_gpu_coverage.py tests/test_gpu_parity.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wide or c3 or hub" ;;
