@@ -652,20 +652,44 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
   const int64_t arow = m0 + i;
   const bool a_ok = arow < M;
   const float* ap = A + (a_ok ? arow : 0) * lda + 4 * h;
+  const uint32_t amask = a_ok ? 0xffffffffu : 0u;  // rows past M contribute +0
   f32x16 acc[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[nt][q] = 0.f;
-  for (int kc = 0; kc < k_pad; kc += 8) {
-    float4 a = a_ok ? *reinterpret_cast<const float4*>(ap + kc) : make_float4(0.f, 0.f, 0.f, 0.f);
+  // D k-steps per iteration: all their loads are issued before their MFMAs (one step per
+  // iteration waited out a full L2 latency per 4 x NT MFMAs).  Steps past k_pad are skipped
+  // (uniform branches), so the MFMA sequence per accumulator is unchanged.
+  constexpr int D = NT == 1 ? 4 : NT == 2 ? 2 : 1;
+  for (int kc = 0; kc < k_pad; kc += 8 * D) {
+    float4 a[D], w[D][NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const float4 w = *reinterpret_cast<const float4*>(W + (int64_t)(nt * 32 + i) * ldw + kc + 4 * h);
-      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w.x, acc[nt], 0, 0, 0);
-      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w.y, acc[nt], 0, 0, 0);
-      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, w.z, acc[nt], 0, 0, 0);
-      acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, w.w, acc[nt], 0, 0, 0);
+    for (int u = 0; u < D; ++u) {
+      const int k = kc + 8 * u;
+      if (k < k_pad) {
+        // ap is row 0 for rows past M: the load stays unconditional, masked to +0 below
+        a[u] = *reinterpret_cast<const float4*>(ap + k);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          w[u][nt] = *reinterpret_cast<const float4*>(W + (int64_t)(nt * 32 + i) * ldw + k + 4 * h);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      if (kc + 8 * u < k_pad) {
+        a[u].x = __uint_as_float(__float_as_uint(a[u].x) & amask);
+        a[u].y = __uint_as_float(__float_as_uint(a[u].y) & amask);
+        a[u].z = __uint_as_float(__float_as_uint(a[u].z) & amask);
+        a[u].w = __uint_as_float(__float_as_uint(a[u].w) & amask);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x, w[u][nt].x, acc[nt], 0, 0, 0);
+          acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y, w[u][nt].y, acc[nt], 0, 0, 0);
+          acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z, w[u][nt].z, acc[nt], 0, 0, 0);
+          acc[nt] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w, w[u][nt].w, acc[nt], 0, 0, 0);
+        }
+      }
     }
   }
 #pragma unroll
@@ -888,7 +912,66 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
 // slice themselves: for small frontiers and many rows (the c5 shape; c3 node_prediction's 128-wide
 // SAGE tables) that re-reads the same table rows from L2 once per mask row.  Same operations per
 // value in the same order as k_agg<true> (bitwise the same h1).
+// One term of k_agg_l1_rows for the wave's 64 rows and W features: s (all 0 on entry) gets the
+// term's value, in k_agg<true>'s operation order.
 template <int W>
+__device__ __forceinline__ void l1_rows_term(const AggArgs& a, int k, int t, int t0, int fo, const float* kb,
+                                             const uint32_t* mrow, float (&s)[W]) {
+  const int kind = a.kind[k];
+  const int r = a.rel[k];
+  const float* __restrict__ T = a.table[k] + fo;
+  const float* __restrict__ selfrow = T + (int64_t)t0 * a.width;
+  if (kind == XPG_TERM_ROOT) {
+#pragma unroll
+    for (int f = 0; f < W; ++f) s[f] = selfrow[f];
+    return;
+  }
+  const float kt = kb[(int64_t)r * a.kpitch + t0];
+  const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+  const int e0 = pp[t], e1 = pp[t + 1];
+  if (kind == XPG_TERM_GCN) {
+    const float dt = inv_sqrt_deg(kt);
+    const float cself = dt * dt;
+#pragma unroll
+    for (int f = 0; f < W; ++f) s[f] = fmaf(cself, selfrow[f], s[f]);
+    for (int e = e0; e < e1; ++e) {  // uniform
+      const int u0 = a.agg_f0[e];
+      const float ku = kb[(int64_t)r * a.kpitch + u0];
+      if (kt >= 0.f && ku >= 0.f) {
+        const float c = inv_sqrt_deg(ku) * dt;
+        const float* __restrict__ src = T + (int64_t)u0 * a.width;
+#pragma unroll
+        for (int f = 0; f < W; ++f) s[f] = fmaf(c, src[f], s[f]);
+      }
+    }
+  } else {  // MEAN
+    const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+    const float cnt = kt + static_cast<float>(sm);
+    if (kt >= 0.f) {
+#pragma unroll
+      for (int f = 0; f < W; ++f) s[f] = fmaf(static_cast<float>(sm), selfrow[f], s[f]);
+    }
+    for (int e = e0; e < e1; ++e) {  // uniform
+      const int u0 = a.agg_f0[e];
+      const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
+      if (keep) {
+        const float* __restrict__ src = (a.rows_blk & 2) ? selfrow : T + (int64_t)u0 * a.width;
+#pragma unroll
+        for (int f = 0; f < W; ++f) s[f] += src[f];
+      }
+    }
+    if (kt >= 0.f) {
+      const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
+#pragma unroll
+      for (int f = 0; f < W; ++f) s[f] *= inv;
+    }
+  }
+}
+
+// ONE (host-checked): term 0 is the only non-ROOT term (SAGE: [MEAN, ROOT]).  Its value then
+// builds in tot itself (0 + s: the generic order's +0 for a -0 sum kept) and the ROOT terms add
+// their rows straight in, so no second W-float array is live: 157 -> ~100 VGPRs at W = 64.
+template <int W, bool ONE>
 __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
   const int64_t wid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -899,70 +982,36 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
   const int64_t wt = wid / nsl;
   const int t = static_cast<int>(wt % a.n_tgt);
   const int64_t b0 = (wt / a.n_tgt) * 64, b = b0 + lane;
-  const bool vrow = b < a.rows;
-  const int64_t bb = vrow ? b : b0;
+  const int64_t bb = b < a.rows ? b : b0;
   const float* kb = a.kin + bb * (int64_t)a.n_rel * a.kpitch;
   const uint32_t* mrow = a.mbits ? a.mbits + bb * a.words : nullptr;
   const int t0 = a.tgt_f0[t];
   float tot[W];
 #pragma unroll
   for (int f = 0; f < W; ++f) tot[f] = 0.f;
-  for (int k = 0; k < a.n_terms; ++k) {
-    const int kind = a.kind[k];
-    const int r = a.rel[k];
-    if (a.tgt_type && a.dst_type[k] >= 0 && a.tgt_type[t] != a.dst_type[k]) continue;  // uniform
-    const float* __restrict__ T = a.table[k] + fo;
-    const float* __restrict__ selfrow = T + (int64_t)t0 * a.width;
-    float s[W];
-    if (kind == XPG_TERM_ROOT) {
+  auto skip = [&](int k) { return a.tgt_type && a.dst_type[k] >= 0 && a.tgt_type[t] != a.dst_type[k]; };
+  if (ONE) {
+    if (!skip(0)) {  // uniform
+      l1_rows_term<W>(a, 0, t, t0, fo, kb, mrow, tot);
 #pragma unroll
-      for (int f = 0; f < W; ++f) s[f] = selfrow[f];
-    } else {
+      for (int f = 0; f < W; ++f) tot[f] = 0.f + tot[f];
+    }
+    for (int k = 1; k < a.n_terms; ++k) {
+      if (skip(k)) continue;  // uniform
+      const float* __restrict__ selfrow = a.table[k] + fo + (int64_t)t0 * a.width;
+#pragma unroll
+      for (int f = 0; f < W; ++f) tot[f] += selfrow[f];
+    }
+  } else {
+    for (int k = 0; k < a.n_terms; ++k) {
+      if (skip(k)) continue;  // uniform
+      float s[W];
 #pragma unroll
       for (int f = 0; f < W; ++f) s[f] = 0.f;
-      const float kt = kb[(int64_t)r * a.kpitch + t0];
-      const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
-      const int e0 = pp[t], e1 = pp[t + 1];
-      if (kind == XPG_TERM_GCN) {
-        const float dt = inv_sqrt_deg(kt);
-        const float cself = dt * dt;
+      l1_rows_term<W>(a, k, t, t0, fo, kb, mrow, s);
 #pragma unroll
-        for (int f = 0; f < W; ++f) s[f] = fmaf(cself, selfrow[f], s[f]);
-        for (int e = e0; e < e1; ++e) {  // uniform
-          const int u0 = a.agg_f0[e];
-          const float ku = kb[(int64_t)r * a.kpitch + u0];
-          if (kt >= 0.f && ku >= 0.f) {
-            const float c = inv_sqrt_deg(ku) * dt;
-            const float* __restrict__ src = T + (int64_t)u0 * a.width;
-#pragma unroll
-            for (int f = 0; f < W; ++f) s[f] = fmaf(c, src[f], s[f]);
-          }
-        }
-      } else {  // MEAN
-        const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
-        const float cnt = kt + static_cast<float>(sm);
-        if (kt >= 0.f) {
-#pragma unroll
-          for (int f = 0; f < W; ++f) s[f] = fmaf(static_cast<float>(sm), selfrow[f], s[f]);
-        }
-        for (int e = e0; e < e1; ++e) {  // uniform
-          const int u0 = a.agg_f0[e];
-          const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
-          if (keep) {
-            const float* __restrict__ src = (a.rows_blk & 2) ? selfrow : T + (int64_t)u0 * a.width;
-#pragma unroll
-            for (int f = 0; f < W; ++f) s[f] += src[f];
-          }
-        }
-        if (kt >= 0.f) {
-          const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
-#pragma unroll
-          for (int f = 0; f < W; ++f) s[f] *= inv;
-        }
-      }
+      for (int f = 0; f < W; ++f) tot[f] += s[f];
     }
-#pragma unroll
-    for (int f = 0; f < W; ++f) tot[f] += s[f];
   }
   // epilogue: bias + activation, then the 64 rows x W tile leaves through this wave's LDS slice
   // in 32-float column chunks, so every store instruction writes whole 128-B lines (8 rows x
@@ -989,7 +1038,6 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
     }
     __builtin_amdgcn_wave_barrier();
   }
-  (void)vrow;
 }
 
 __global__ void k_take_col(const float* __restrict__ C, int64_t M, int64_t ldc, int col,
@@ -2775,7 +2823,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     // 3 = + keep words, 4 = + the first kept rows and the own row (the current target)
     int q1_b0 = 0, q1_b1 = 0, q1_tf0 = 0, q1_tp = 0, q1_sm = 0;
     int q2_b0 = 0, q2_b1 = 0, q2_tf0 = 0, q2_tp = 0, q2_sm = 0, q2_src = 0, q2_u0 = 0;
-    int q3_b0 = 0, q3_b1 = 0, q3_tp = 0, q3_sm = 0, q3_src = 0, q3_u0 = 0;
+    int q3_b0 = 0, q3_b1 = 0, q3_tp = 0, q3_sm = 0, q3_src = 0;
     uint32_t q3_mv = 0u, q3_em = 0u;
     int q4_b0 = 0, q4_b1 = 0, q4_sm = 0, q4_src = 0, q4_cnt = 0;
     uint32_t q4_rest = 0u;
@@ -2799,7 +2847,7 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
     };
     auto st3 = [&](int k) {
       if (k >= ntgt_wg) return;
-      q3_b0 = q2_b0; q3_b1 = q2_b1; q3_tp = q2_tp; q3_sm = q2_sm; q3_src = q2_src; q3_u0 = q2_u0;
+      q3_b0 = q2_b0; q3_b1 = q2_b1; q3_tp = q2_tp; q3_sm = q2_sm; q3_src = q2_src;
       q3_mv = a.mT0[q2_tf0];
       q3_em = q2_b0 + gl < q2_b1 ? a.mT0[q2_u0] : 0u;
     };
@@ -4901,8 +4949,12 @@ int launch_agg(const AggArgs& a, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
     AggArgs b = a;
     if (const int rc = diag_env("XPG_L1_DBG", &b.rows_blk)) return rc;
-    if (slice == 64) hipLaunchKernelGGL(k_agg_l1_rows<64>, grid, block, 0, st, b);
-    else hipLaunchKernelGGL(k_agg_l1_rows<32>, grid, block, 0, st, b);
+    bool one = a.kind[0] != XPG_TERM_ROOT;
+    for (int k = 1; k < a.n_terms; ++k) one = one && a.kind[k] == XPG_TERM_ROOT;
+    if (slice == 64 && one) hipLaunchKernelGGL((k_agg_l1_rows<64, true>), grid, block, 0, st, b);
+    else if (slice == 64) hipLaunchKernelGGL((k_agg_l1_rows<64, false>), grid, block, 0, st, b);
+    else if (one) hipLaunchKernelGGL((k_agg_l1_rows<32, true>), grid, block, 0, st, b);
+    else hipLaunchKernelGGL((k_agg_l1_rows<32, false>), grid, block, 0, st, b);
     XPG_LAUNCHED();
     return XPG_OK;
   }
