@@ -776,7 +776,7 @@ struct AggArgs {
   int kpitch;
   const uint32_t* mbits;
   const int32_t* f0_node;
-  int rows_blk;  // (diagnostics, XPG_L1_DBG) k_agg_l1_rows: 1 every source kept, 2 every source = the self row
+  int rows_blk;  // (diagnostics, XPG_L1_DBG) k_agg_l1_rows: 1 every source kept, 2 every source = the self row, 4 no output stores
 };
 
 __device__ __forceinline__ float inv_sqrt_deg(float kin) {
@@ -904,6 +904,70 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
   }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// One term of k_agg_l1_rows for the wave's 64 rows and W features: s (all 0 on entry) gets the
+// term's value, in k_agg<true>'s operation order.  Features are handled in pairs (f32x2: packed
+// fp32 add / fma / mul, two features per VALU instruction; each lane's operations per feature are
+// unchanged).
+template <int W>
+__device__ __forceinline__ void l1_rows_term(const AggArgs& a, int k, int t, int t0, int fo, const float* kb,
+                                             const uint32_t* mrow, f32x2 (&s)[W / 2]) {
+  const int kind = a.kind[k];
+  const int r = a.rel[k];
+  const float* __restrict__ T = a.table[k] + fo;
+  const f32x2* __restrict__ selfrow = reinterpret_cast<const f32x2*>(T + (int64_t)t0 * a.width);
+  if (kind == XPG_TERM_ROOT) {
+#pragma unroll
+    for (int j = 0; j < W / 2; ++j) s[j] = selfrow[j];
+    return;
+  }
+  const float kt = kb[(int64_t)r * a.kpitch + t0];
+  const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
+  const int e0 = pp[t], e1 = pp[t + 1];
+  if (kind == XPG_TERM_GCN) {
+    const float dt = inv_sqrt_deg(kt);
+    const f32x2 cself = dt * dt;
+#pragma unroll
+    for (int j = 0; j < W / 2; ++j) s[j] = fma2(cself, selfrow[j], s[j]);
+    for (int e = e0; e < e1; ++e) {  // uniform
+      const int u0 = a.agg_f0[e];
+      const float ku = kb[(int64_t)r * a.kpitch + u0];
+      if (kt >= 0.f && ku >= 0.f) {
+        const f32x2 c = inv_sqrt_deg(ku) * dt;
+        const f32x2* __restrict__ src = reinterpret_cast<const f32x2*>(T + (int64_t)u0 * a.width);
+#pragma unroll
+        for (int j = 0; j < W / 2; ++j) s[j] = fma2(c, src[j], s[j]);
+      }
+    }
+  } else {  // MEAN
+    const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
+    const float cnt = kt + static_cast<float>(sm);
+    if (kt >= 0.f) {
+      const f32x2 smf = static_cast<float>(sm);
+#pragma unroll
+      for (int j = 0; j < W / 2; ++j) s[j] = fma2(smf, selfrow[j], s[j]);
+    }
+    for (int e = e0; e < e1; ++e) {  // uniform
+      const int u0 = a.agg_f0[e];
+      const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
+      if (keep) {
+        const f32x2* __restrict__ src =
+            (a.rows_blk & 2) ? selfrow : reinterpret_cast<const f32x2*>(T + (int64_t)u0 * a.width);
+#pragma unroll
+        for (int j = 0; j < W / 2; ++j) s[j] += src[j];
+      }
+    }
+    if (kt >= 0.f) {
+      const f32x2 inv = 1.f / (cnt > 1.f ? cnt : 1.f);
+#pragma unroll
+      for (int j = 0; j < W / 2; ++j) s[j] *= inv;
+    }
+  }
+}
+
 // Layer-1 aggregation with lanes = mask rows (no edge masks): wave = (block of 64 mask rows, one
 // target, one W-feature slice of the layer's a.width = W, 2W, 4W features).  The tables are shared
 // by every mask row, so each in-edge's table slice is a wave-uniform read (scalar loads) added to
@@ -912,65 +976,9 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
 // slice themselves: for small frontiers and many rows (the c5 shape; c3 node_prediction's 128-wide
 // SAGE tables) that re-reads the same table rows from L2 once per mask row.  Same operations per
 // value in the same order as k_agg<true> (bitwise the same h1).
-// One term of k_agg_l1_rows for the wave's 64 rows and W features: s (all 0 on entry) gets the
-// term's value, in k_agg<true>'s operation order.
-template <int W>
-__device__ __forceinline__ void l1_rows_term(const AggArgs& a, int k, int t, int t0, int fo, const float* kb,
-                                             const uint32_t* mrow, float (&s)[W]) {
-  const int kind = a.kind[k];
-  const int r = a.rel[k];
-  const float* __restrict__ T = a.table[k] + fo;
-  const float* __restrict__ selfrow = T + (int64_t)t0 * a.width;
-  if (kind == XPG_TERM_ROOT) {
-#pragma unroll
-    for (int f = 0; f < W; ++f) s[f] = selfrow[f];
-    return;
-  }
-  const float kt = kb[(int64_t)r * a.kpitch + t0];
-  const int* pp = a.agg_ptr + (int64_t)r * (a.n_tgt + 1);
-  const int e0 = pp[t], e1 = pp[t + 1];
-  if (kind == XPG_TERM_GCN) {
-    const float dt = inv_sqrt_deg(kt);
-    const float cself = dt * dt;
-#pragma unroll
-    for (int f = 0; f < W; ++f) s[f] = fmaf(cself, selfrow[f], s[f]);
-    for (int e = e0; e < e1; ++e) {  // uniform
-      const int u0 = a.agg_f0[e];
-      const float ku = kb[(int64_t)r * a.kpitch + u0];
-      if (kt >= 0.f && ku >= 0.f) {
-        const float c = inv_sqrt_deg(ku) * dt;
-        const float* __restrict__ src = T + (int64_t)u0 * a.width;
-#pragma unroll
-        for (int f = 0; f < W; ++f) s[f] = fmaf(c, src[f], s[f]);
-      }
-    }
-  } else {  // MEAN
-    const int sm = a.self_mult[(int64_t)r * a.n_tgt + t];
-    const float cnt = kt + static_cast<float>(sm);
-    if (kt >= 0.f) {
-#pragma unroll
-      for (int f = 0; f < W; ++f) s[f] = fmaf(static_cast<float>(sm), selfrow[f], s[f]);
-    }
-    for (int e = e0; e < e1; ++e) {  // uniform
-      const int u0 = a.agg_f0[e];
-      const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
-      if (keep) {
-        const float* __restrict__ src = (a.rows_blk & 2) ? selfrow : T + (int64_t)u0 * a.width;
-#pragma unroll
-        for (int f = 0; f < W; ++f) s[f] += src[f];
-      }
-    }
-    if (kt >= 0.f) {
-      const float inv = 1.f / (cnt > 1.f ? cnt : 1.f);
-#pragma unroll
-      for (int f = 0; f < W; ++f) s[f] *= inv;
-    }
-  }
-}
-
 // ONE (host-checked): term 0 is the only non-ROOT term (SAGE: [MEAN, ROOT]).  Its value then
 // builds in tot itself (0 + s: the generic order's +0 for a -0 sum kept) and the ROOT terms add
-// their rows straight in, so no second W-float array is live: 157 -> ~100 VGPRs at W = 64.
+// their rows straight in, so no second W-float array is live: 157 -> 111 VGPRs at W = 64.
 template <int W, bool ONE>
 __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
   const int64_t wid = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -986,32 +994,38 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
   const float* kb = a.kin + bb * (int64_t)a.n_rel * a.kpitch;
   const uint32_t* mrow = a.mbits ? a.mbits + bb * a.words : nullptr;
   const int t0 = a.tgt_f0[t];
-  float tot[W];
+  f32x2 tot2[W / 2];
 #pragma unroll
-  for (int f = 0; f < W; ++f) tot[f] = 0.f;
+  for (int j = 0; j < W / 2; ++j) tot2[j] = 0.f;
   auto skip = [&](int k) { return a.tgt_type && a.dst_type[k] >= 0 && a.tgt_type[t] != a.dst_type[k]; };
   if (ONE) {
     if (!skip(0)) {  // uniform
-      l1_rows_term<W>(a, 0, t, t0, fo, kb, mrow, tot);
+      l1_rows_term<W>(a, 0, t, t0, fo, kb, mrow, tot2);
 #pragma unroll
-      for (int f = 0; f < W; ++f) tot[f] = 0.f + tot[f];
+      for (int j = 0; j < W / 2; ++j) tot2[j] = 0.f + tot2[j];
     }
     for (int k = 1; k < a.n_terms; ++k) {
       if (skip(k)) continue;  // uniform
-      const float* __restrict__ selfrow = a.table[k] + fo + (int64_t)t0 * a.width;
+      const f32x2* __restrict__ selfrow = reinterpret_cast<const f32x2*>(a.table[k] + fo + (int64_t)t0 * a.width);
 #pragma unroll
-      for (int f = 0; f < W; ++f) tot[f] += selfrow[f];
+      for (int j = 0; j < W / 2; ++j) tot2[j] += selfrow[j];
     }
   } else {
     for (int k = 0; k < a.n_terms; ++k) {
       if (skip(k)) continue;  // uniform
-      float s[W];
+      f32x2 s[W / 2];
 #pragma unroll
-      for (int f = 0; f < W; ++f) s[f] = 0.f;
+      for (int j = 0; j < W / 2; ++j) s[j] = 0.f;
       l1_rows_term<W>(a, k, t, t0, fo, kb, mrow, s);
 #pragma unroll
-      for (int f = 0; f < W; ++f) tot[f] += s[f];
+      for (int j = 0; j < W / 2; ++j) tot2[j] += s[j];
     }
+  }
+  float tot[W];
+#pragma unroll
+  for (int j = 0; j < W / 2; ++j) {
+    tot[2 * j] = tot2[j].x;
+    tot[2 * j + 1] = tot2[j].y;
   }
   // epilogue: bias + activation, then the 64 rows x W tile leaves through this wave's LDS slice
   // in 32-float column chunks, so every store instruction writes whole 128-B lines (8 rows x
@@ -1033,7 +1047,7 @@ __global__ __launch_bounds__(256) void k_agg_l1_rows(AggArgs a) {
       const int row = rr + 8 * i;
       const float* src = tile + row * 33 + 4 * q;
       const float4 v = make_float4(src[0], src[1], src[2], src[3]);
-      if (b0 + row < a.rows)
+      if (b0 + row < a.rows && !(a.rows_blk & 4))
         *reinterpret_cast<float4*>(a.out + ((b0 + row) * a.n_tgt + t) * a.out_ld + fo + 32 * c + 4 * q) = v;
     }
     __builtin_amdgcn_wave_barrier();

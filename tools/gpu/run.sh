@@ -60,8 +60,8 @@ for step in "$@"; do
            run pmc_write_c3 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 ;;
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
     # k_agg_l1_rows ablations on the rows_ab plans (XPG_L1_DBG 1: no keep loads, 2: every source
-    # the self row, 3: both; outputs invalid) + the kernel stats of the unablated run
-    l1abl) for d in 0 1 2 3; do XPG_DIAGNOSTICS=1 XPG_L1_DBG=$d run l1abl_$d 200 python -u tools/rows_ab.py || exit 1; done && \
+    # the self row, 4: no output stores, or-ed; outputs invalid) + the kernel stats of the unablated run
+    l1abl) for d in 0 1 2 3 4 7; do XPG_DIAGNOSTICS=1 XPG_L1_DBG=$d run l1abl_$d 200 python -u tools/rows_ab.py || exit 1; done && \
            cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run rowsprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rowsprof -o run -- python3 tools/rows_ab.py ;;
     apiprof3) run apiprof3 300 python -u tools/api_profile.py --graph c3 && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
