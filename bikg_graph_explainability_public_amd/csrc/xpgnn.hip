@@ -85,6 +85,9 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int words_of(int64_t cols) { return static_cast<int>((cols + 31) / 32); }
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup fence on every address
 // space: it waits for vmcnt(0), i.e. for every global load still in flight (prefetches of the
@@ -903,10 +906,6 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
     }
   }
 }
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // One term of k_agg_l1_rows for the wave's 64 rows and W features: s (all 0 on entry) gets the
 // term's value, in k_agg<true>'s operation order.  Features are handled in pairs (f32x2: packed

@@ -5,6 +5,7 @@ one 32-row pass per variant; outputs compared with the exact f32 variant (XPG_WI
     python tools/ws_ab.py [--nodes N] [--edges E] [--variants "B3=0;B3=1;OVERLAP=0"]
 """
 import argparse
+import hashlib
 import os
 import sys
 import time
@@ -79,8 +80,8 @@ def main():
             first = y.clone()
         d1 = float((y - first).abs().max())
         print(f"[{spec:>18s}] {args.rows} rows: {ms:8.3f} ms  layer1 {l1:7.3f} layer2 {l2:7.3f} ms/pass  "
-              f"max|y - y_exact| = {d:.3e}  max|y - y_first| = {d1:.3e}  bitwise_first={bool(torch.equal(y, first))}",
-              flush=True)
+              f"max|y - y_exact| = {d:.3e}  max|y - y_first| = {d1:.3e}  bitwise_first={bool(torch.equal(y, first))}  "
+              f"y hash {hashlib.sha1(y.cpu().numpy().tobytes()).hexdigest()[:16]}", flush=True)
     set_env("")
 
 
