@@ -626,6 +626,18 @@ __global__ void k_shap_clean(int64_t rows, double* __restrict__ out) {
   if (r < rows) out[r] = clean_inf(out[r]);
 }
 
+// Sum over the 32 lanes of each half of the wave (lanes l and l ^ 32 keep separate sums), on the
+// VALU: quad DPP (xor 1, xor 2), row_ror 4 and 8 inside 16-lane rows, then v_permlane16_swap for
+// the two rows of the half.  Every lane of the half ends with the same total.
+__device__ __forceinline__ float half_wave_sum(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));  // row_ror:4
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ------------------------------------------------------------------------------------ dense
 // C = act(A W^T + b) on v_mfma_f32_32x32x2_f32.  One wave owns 32 rows x (NT*32) columns
 // (column group cg of n_groups: consecutive waves take the column groups of one 32-row block, so
@@ -634,13 +646,21 @@ __global__ void k_shap_clean(int64_t rows, double* __restrict__ out) {
 // float4 of each W row, feeding 4 MFMAs whose 2 k-slots map to k = kc + 4*h + s (h = lane >> 5),
 // identically for A and B, so the contraction is exact.  C/D map: col = lane & 31,
 // row = (reg & 3) + 8 * (reg >> 2) + 4 * h.
-template <int NT>
+// HEAD: the network's output column is one more linear layer of this one, y[m] =
+// hact(sum_c v[m][c] hw[c] + hb[0]) over this layer's outputs v (bias + activation applied, padding
+// columns 0).  v is not stored: each lane multiplies its column's values by hw, the 32 columns of a
+// tile are summed across the half-wave, the column groups of a 32-row block (the workgroup's 4
+// waves when n_groups = 4) add their partials in group order through LDS.  This replaces the
+// 1-column head's own dense launch (a 32-wide padded tile) and the column pick.
+template <int NT, bool HEAD = false>
 __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int64_t M, int64_t lda,
                                                const float* __restrict__ W, int64_t ldw, int k_pad,
                                                const float* __restrict__ bias, int n_real, int act,
                                                float* __restrict__ C, int64_t ldc,
                                                const int32_t* __restrict__ row_type, int64_t type_mod,
-                                               int bias_ld, int n_groups) {
+                                               int bias_ld, int n_groups, const float* __restrict__ hw = nullptr,
+                                               const float* __restrict__ hb = nullptr, int hact = 0,
+                                               float* __restrict__ y = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t wv = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
   const int cg = static_cast<int>(wv % n_groups);
@@ -650,6 +670,7 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
   W += (int64_t)c0 * ldw;
   bias += c0;
   C += c0;
+  if (HEAD) hw += c0;
   n_real -= c0;
   const int i = lane & 31, h = lane >> 5;
   const int64_t arow = m0 + i;
@@ -695,17 +716,46 @@ __global__ __launch_bounds__(256) void k_dense(const float* __restrict__ A, int6
       }
     }
   }
+  float part[HEAD ? 16 : 1];
+  if (HEAD) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) part[reg] = 0.f;
+  }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int col = nt * 32 + i;
     const float bv = col < n_real ? bias[col] : 0.f;
+    const float hwc = HEAD && col < n_real ? hw[col] : 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int64_t m = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
       // multi-node-type layers: the bias of the row's target type (rows are (mask row, target))
       const float b = (row_type && m < M && col < n_real) ? bias[(int64_t)row_type[m % type_mod] * bias_ld + col]
                                                           : bv;
-      if (m < M) C[m * ldc + col] = col < n_real ? act_apply(acc[nt][reg] + b, act) : 0.f;
+      const float v = col < n_real ? act_apply(acc[nt][reg] + b, act) : 0.f;
+      if (HEAD) part[reg] = fmaf(v, hwc, part[reg]);
+      else if (m < M) C[m * ldc + col] = v;
+    }
+  }
+  if (HEAD) {
+    __shared__ float hp[4][32];  // [wave][row of the 32-row block]
+    const int wl = threadIdx.x >> 6;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) part[reg] = half_wave_sum(part[reg]);
+    if (i == 0) {  // lanes 0 and 32: the totals of their half's 16 rows
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) hp[wl][(reg & 3) + 8 * (reg >> 2) + 4 * h] = part[reg];
+    }
+    if (n_groups > 1) {
+      __syncthreads();  // the workgroup's waves are the n_groups column groups of one block
+      if (cg != 0) return;
+    } else {
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < 32 && m0 + lane < M) {
+      float t = hp[wl][lane];
+      for (int g = 1; g < n_groups; ++g) t += hp[wl + g][lane];
+      y[m0 + lane] = act_apply(t + hb[0], hact);
     }
   }
 }
@@ -2014,17 +2064,6 @@ __device__ __forceinline__ void wide_gather2(const WideArgs& a, int e0, int e1, 
 }
 
 
-// Sum over the 32 lanes of each half of the wave (lanes l and l ^ 32 keep separate sums), on the
-// VALU: quad DPP (xor 1, xor 2), row_ror 4 and 8 inside 16-lane rows, then v_permlane16_swap for
-// the two rows of the half.  Every lane of the half ends with the same total.
-__device__ __forceinline__ float half_wave_sum(float x) {
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));  // row_ror:4
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));  // row_ror:8
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
 
 
 
@@ -4921,9 +4960,19 @@ int layout_ws(const xpg_forward_plan* p, int64_t rows, WsLayout* L) {
   return XPG_OK;
 }
 
+// OutColumn: the output column of the network's last dense layer computed in this launch's
+// epilogue (k_dense HEAD): y[m] = act(sum_c v[m][c] w[c] + b[0])
+struct OutColumn {
+  const float* w = nullptr;  // the output column's weight row (the layer's k_pad entries)
+  const float* b = nullptr;  // its bias (one float)
+  int act = 0;
+  float* y = nullptr;
+};
+
 int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t ldw, int64_t k_pad,
                  const float* bias, int64_t n_real, int64_t n_pad, int act, float* C, int64_t ldc,
-                 hipStream_t st, const int32_t* row_type = nullptr, int64_t type_mod = 1, int bias_ld = 0) {
+                 hipStream_t st, const int32_t* row_type = nullptr, int64_t type_mod = 1, int bias_ld = 0,
+                 const OutColumn* head = nullptr) {
   XPG_REQ(k_pad % 8 == 0 && n_pad % 32 == 0 && n_pad >= 32 && n_pad <= 256,
           "xpg_dense: k_pad % 8, n_pad in {32..256} step 32 required");
   XPG_REQ(lda % 4 == 0 && ldw % 4 == 0, "xpg_dense: lda/ldw must be multiples of 4");
@@ -4936,9 +4985,15 @@ int launch_dense(const float* A, int64_t M, int64_t lda, const float* W, int64_t
   dim3 grid(static_cast<unsigned>(cdiv(waves, 4))), block(256);
   const int kp = static_cast<int>(k_pad), nr = static_cast<int>(n_real);
   switch (tiles / groups) {
-#define XPG_DENSE_CASE(NT) \
-    case NT: hipLaunchKernelGGL(k_dense<NT>, grid, block, 0, st, A, M, lda, W, ldw, kp, bias, nr, act, C, ldc, \
-                                row_type, type_mod, bias_ld, groups); break;
+#define XPG_DENSE_CASE(NT)                                                                                      \
+    case NT:                                                                                                    \
+      if (head)                                                                                                 \
+        hipLaunchKernelGGL((k_dense<NT, true>), grid, block, 0, st, A, M, lda, W, ldw, kp, bias, nr, act, C,   \
+                           ldc, row_type, type_mod, bias_ld, groups, head->w, head->b, head->act, head->y);     \
+      else                                                                                                      \
+        hipLaunchKernelGGL((k_dense<NT, false>), grid, block, 0, st, A, M, lda, W, ldw, kp, bias, nr, act, C,  \
+                           ldc, row_type, type_mod, bias_ld, groups, nullptr, nullptr, 0, nullptr);             \
+      break;
     XPG_DENSE_CASE(1) XPG_DENSE_CASE(2) XPG_DENSE_CASE(3) XPG_DENSE_CASE(4)
     XPG_DENSE_CASE(5) XPG_DENSE_CASE(6) XPG_DENSE_CASE(7) XPG_DENSE_CASE(8)
 #undef XPG_DENSE_CASE
@@ -6009,6 +6064,22 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   float* kin = reinterpret_cast<float*>(ws + L.kin);
   const int words = words_of(p->cols);
   const int kpitch = deg_pitch(p);
+  // The picked output column is fused into the last dense layer's epilogue (k_dense HEAD) when the
+  // network ends in a head layer that follows a dense layer (another head layer, or a conv layer
+  // past the first) and no link decoder: no 32-wide padded head tile, no column pick.
+  OutColumn fh;
+  bool fuse_out = false;
+  if (!p->edge_dot && p->n_head >= 1 && (p->n_head >= 2 || p->n_layers >= 2)) {
+    const xpg_head_desc& hl = p->head[p->n_head - 1];
+    const int64_t prev_pad = p->n_head >= 2 ? p->head[p->n_head - 2].n_pad : p->layers[p->n_layers - 1].f_out_pad;
+    if (hl.k_pad == prev_pad && p->out_col >= 0 && p->out_col < hl.n_real) {
+      fuse_out = true;
+      fh.w = hl.weight + (int64_t)p->out_col * hl.k_pad;
+      fh.b = hl.bias + p->out_col;
+      fh.act = hl.act;
+      fh.y = y;
+    }
+  }
   {
     const int64_t n = rows * (int64_t)p->n_rel * kpitch;
     XPG_REQ(!p->edge_masks || p->deg_eid || p->n_deg_edges == 0, "masked_forward: edge-mask plan without deg_eid");
@@ -6077,8 +6148,10 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
       a.out_ld = (int64_t)ly.n_terms * ly.f_in_pad;
       rc = launch_agg<false>(a, st);
       if (rc) return rc;
+      const bool fuse_here = fuse_out && p->n_head == 1 && l == p->n_layers - 1;
       rc = launch_dense(agg, rows * ly.n_tgt, a.out_ld, ly.weight, a.out_ld, a.out_ld, ly.bias, ly.f_out,
-                        ly.f_out_pad, ly.act, hout, ly.f_out_pad, st, ly.tgt_type, ly.n_tgt, ly.f_out_pad);
+                        ly.f_out_pad, ly.act, hout, ly.f_out_pad, st, ly.tgt_type, ly.n_tgt, ly.f_out_pad,
+                        fuse_here ? &fh : nullptr);
       if (rc) return rc;
     }
   }
@@ -6086,16 +6159,18 @@ int xpg_masked_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t 
   const int64_t M = rows * last.n_tgt;
   const float* cur = reinterpret_cast<const float*>(ws + L.h[p->n_layers - 1]);
   int64_t cur_ld = last.f_out_pad;
-  for (int i = 0; i < p->n_head; ++i) {
+  const int n_head_launch = p->n_head - (fuse_out ? 1 : 0);  // the last head layer fused (fh)
+  for (int i = 0; i < n_head_launch; ++i) {
     const xpg_head_desc& hd = p->head[i];
     XPG_REQ(hd.k_pad == cur_ld, "head: k_pad must equal the previous padded width");
     float* nxt = reinterpret_cast<float*>(ws + ((i & 1) ? L.head1 : L.head0));
     rc = launch_dense(cur, M, cur_ld, hd.weight, hd.k_pad, hd.k_pad, hd.bias, hd.n_real, hd.n_pad, hd.act, nxt,
-                      hd.n_pad, st);
+                      hd.n_pad, st, nullptr, 1, 0, fuse_out && i == n_head_launch - 1 ? &fh : nullptr);
     if (rc) return rc;
     cur = nxt;
     cur_ld = hd.n_pad;
   }
+  if (fuse_out) return XPG_OK;
   if (p->edge_dot) {
     const int n_real = p->n_head > 0 ? p->head[p->n_head - 1].n_real : last.f_out;
     XPG_REQ(p->dot_a >= 0 && p->dot_a < last.n_tgt && p->dot_b >= 0 && p->dot_b < last.n_tgt,
