@@ -913,16 +913,55 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs a) {
           const float cnt = kt + static_cast<float>(sm);
 #pragma unroll
           for (int j = 0; j < NV; ++j) fma4(s[j], static_cast<float>(sm), selfrow[sub + j * LPS]);
-          for (int e = pp[t]; e < pp[t + 1]; ++e) {
-            const int u0 = a.agg_f0[e];
-            if (brow ? bit_of(brow, a.agg_eid[e])
-                     : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f) {
-              const int up = L1 ? u0 : a.agg_src[e];
-              const float4* src = reinterpret_cast<const float4*>(base + (int64_t)up * a.width);
+          // EB in-edges at a time: their keep tests, then the kept sources' rows, are all issued
+          // before the first add (one edge at a time each edge waited out its whole
+          // edge -> keep word -> row chain); the adds stay in edge order
+          constexpr int EB = NV >= 4 ? 2 : NV == 2 ? 4 : 8;
+          const int e_end = pp[t + 1];
+          for (int eb = pp[t]; eb < e_end; eb += EB) {
+            bool kp[EB];
+            int up[EB], kx[EB];
+            // stage by stage over the EB edges (the keep source is uniform: edge bits, the
+            // source's own mask bit, or its kin entry), so each stage's loads go out together
 #pragma unroll
-              for (int j = 0; j < NV; ++j) {
-                const float4 v = src[sub + j * LPS];
-                s[j].x += v.x; s[j].y += v.y; s[j].z += v.z; s[j].w += v.w;
+            for (int q = 0; q < EB; ++q) {
+              const int e = eb + q < e_end ? eb + q : eb;
+              up[q] = a.agg_f0[e];
+              kx[q] = brow ? a.agg_eid[e] : 0;
+            }
+            if (brow) {
+#pragma unroll
+              for (int q = 0; q < EB; ++q) kp[q] = bit_of(brow, kx[q]);
+            } else if (mrow) {
+#pragma unroll
+              for (int q = 0; q < EB; ++q) kx[q] = a.f0_node[up[q]];
+#pragma unroll
+              for (int q = 0; q < EB; ++q) kp[q] = bit_of(mrow, kx[q]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < EB; ++q) kp[q] = kb[(int64_t)r * a.kpitch + up[q]] >= 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < EB; ++q) {
+              kp[q] = kp[q] && eb + q < e_end;
+              if (!L1) up[q] = a.agg_src[eb + q < e_end ? eb + q : eb];
+            }
+#pragma unroll
+            for (int q = 0; q < EB; ++q) asm volatile("" ::"v"(up[q]));  // issued here, not sunk into the branches
+            float4 v[EB][NV];
+#pragma unroll
+            for (int q = 0; q < EB; ++q) {
+              const float4* src = reinterpret_cast<const float4*>(base + (int64_t)up[q] * a.width);
+#pragma unroll
+              for (int j = 0; j < NV; ++j) v[q][j] = kp[q] ? src[sub + j * LPS] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int q = 0; q < EB; ++q) {
+              if (kp[q]) {
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                  s[j].x += v[q][j].x; s[j].y += v[q][j].y; s[j].z += v[q][j].z; s[j].w += v[q][j].w;
+                }
               }
             }
           }
