@@ -1038,14 +1038,33 @@ __device__ __forceinline__ void l1_rows_term(const AggArgs& a, int k, int t, int
 #pragma unroll
       for (int j = 0; j < W / 2; ++j) s[j] = fma2(smf, selfrow[j], s[j]);
     }
-    for (int e = e0; e < e1; ++e) {  // uniform
-      const int u0 = a.agg_f0[e];
-      const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : mrow ? bit_of(mrow, a.f0_node[u0]) : kb[(int64_t)r * a.kpitch + u0] >= 0.f);
-      if (keep) {
-        const f32x2* __restrict__ src =
-            (a.rows_blk & 2) ? selfrow : reinterpret_cast<const f32x2*>(T + (int64_t)u0 * a.width);
+    // 8 in-edges at a time: their sources and keep words are loaded stage by stage before the
+    // first add (one edge at a time each edge waited out its edge -> node -> keep word chain)
+    for (int eb = e0; eb < e1; eb += 8) {  // uniform
+      int uu[8];
+      bool kw[8];
 #pragma unroll
-        for (int j = 0; j < W / 2; ++j) s[j] += src[j];
+      for (int q = 0; q < 8; ++q) uu[q] = a.agg_f0[eb + q < e1 ? eb + q : eb];
+      if (mrow) {
+        int nd[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nd[q] = a.f0_node[uu[q]];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) kw[q] = bit_of(mrow, nd[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) kw[q] = kb[(int64_t)r * a.kpitch + uu[q]] >= 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (eb + q >= e1) break;  // uniform
+        const bool keep = kt >= 0.f && ((a.rows_blk & 1) ? true : kw[q]);
+        if (keep) {
+          const f32x2* __restrict__ src =
+              (a.rows_blk & 2) ? selfrow : reinterpret_cast<const f32x2*>(T + (int64_t)uu[q] * a.width);
+#pragma unroll
+          for (int j = 0; j < W / 2; ++j) s[j] += src[j];
+        }
       }
     }
     if (kt >= 0.f) {
