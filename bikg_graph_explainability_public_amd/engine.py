@@ -486,21 +486,30 @@ def plan_arrays_numpy(S, rel_np, queries, L, rel_eid=None):
             "deg_eid": deg_eid, "layers": layers}
 
 
-_STAGING = {}  # device index -> (pinned host tensor, event of its last copy)
+_STAGING = {}  # device index -> [next slot, [(pinned host tensor, event of its last copy)] * _STAGING_SLOTS]
 _STAGING_MAX = 16 << 20  # bytes: larger arrays take the pageable copy
+_STAGING_SLOTS = 4  # a call's uploads take consecutive slots: none waits for the previous copy
 
 
 def h2d(a, device):
     """A host numpy array (int32 / int64 / float32) as a new device tensor, copied from a pinned
     staging buffer without a host wait: a pageable host -> device copy waits for everything queued
     on the stream first (~40 us of an Explainer.run first call per plan upload, the device idle
-    meanwhile).  The buffer is reused once its previous copy has completed (its event)."""
+    meanwhile).  Uploads rotate over a few pinned buffers; a buffer is reused once its previous
+    copy has completed (its event: with one buffer the second upload of a call waited for the
+    first copy, i.e. for everything queued before it)."""
     a = np.ascontiguousarray(a)
     dev = torch.device(device)
     if a.nbytes > _STAGING_MAX or a.nbytes == 0:
         return torch.from_numpy(a).to(dev)
     key = dev.index if dev.index is not None else torch.cuda.current_device()
-    buf, ev = _STAGING.get(key, (None, None))
+    ring = _STAGING.get(key)
+    if ring is None:  # every slot pinned up front: a pinned allocation costs ~0.2 ms per call
+        ring = _STAGING[key] = [0, [(torch.empty(1 << 20, dtype=torch.uint8, pin_memory=True), None)
+                                    for _ in range(_STAGING_SLOTS)]]
+    slot = ring[0]
+    ring[0] = (slot + 1) % _STAGING_SLOTS
+    buf, ev = ring[1][slot]
     if ev is not None:
         ev.synchronize()
     if buf is None or buf.numel() < a.nbytes:
@@ -510,7 +519,7 @@ def h2d(a, device):
     out.view(-1).view(torch.uint8).copy_(buf[:a.nbytes], non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
-    _STAGING[key] = (buf, ev)
+    ring[1][slot] = (buf, ev)
     return out
 
 
