@@ -853,6 +853,10 @@ def c3_section(args, dev, world, rank):
     kt = engine.profile_read()
     engine.profile_enable(False)
     assert logits.shape == (total, qcols.numel())
+    # bitwise fingerprint of the gathered query-column logits (the 2-rank rehearsal compares it
+    # with a 1-rank run: sharding + all-gather must not change a bit)
+    import hashlib
+    checksum = hashlib.sha256(logits.float().cpu().numpy().tobytes()).hexdigest()[:16]
     # per row: kept edges (both endpoints active) and active nodes, for the byte counts
     kept, act = [], []
     for c0 in range(0, r1 - r0, 32):
@@ -918,7 +922,8 @@ def c3_section(args, dev, world, rank):
                     "Linear(128,1) + sigmoid, every node a target (all 1M outputs per mask row), "
                     f"{total} mask rows sharded over {world} rank(s) in 32-row passes, then an "
                     "all-gather of 64 query columns of every row",
-        "rows": total, "rows_per_rank": rows_rank, "ms": wall * 1e3,
+        "rows": total, "rows_per_rank": rows_rank, "logits_checksum": checksum,
+        "ms": wall * 1e3,
         "forward_ms_rank0": fwd_ms, "pass_ms_rank0": fwd_ms / max(1, npass),
         "samples_per_s": total / wall,
         "samples_per_s_per_rank": rows_rank / (fwd_ms * 1e-3),
@@ -1561,6 +1566,99 @@ def explainer_section(args, dev):
     return out
 
 
+# ----------------------------------------------------------------------------- north star
+BF16_MFMA_PEAK_TF = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense BF16 MFMA
+
+
+def sq_file(section):
+    """profiles/sq_<section>.json (tools/sq_json.py: SQ / GRBM counters per exact kernel
+    instantiation from one rocprofv3 PMC pass), or {}."""
+    fn = os.path.join(ROOT, "profiles", f"sq_{section}.json")
+    return json.load(open(fn)) if os.path.exists(fn) else {}
+
+
+def north_star_block(c3):
+    """The north-star evidence (BASELINE.json: >= 40 % HBM roofline on the masked message-passing
+    gather at 1 GPU, MFMA utilisation against chip peak) as a compact block for the headline's
+    `roofline`: the c3 full-graph pass (configs[2], SURVEY.md §8d regime (ii)) per kernel —
+    live ms and algorithmic-byte fraction, the counter-byte fraction (profiles/pmc_c3.json), the
+    exact-f32 layer 2 beside the default three-piece bf16 one, and the MFMA pipe: busy fraction
+    from SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / 8) (profiles/sq_c3.json) and the
+    live bf16 MFMA rate of the layer-2 products against the dense bf16 peak."""
+    ks = c3["kernels"]
+    l1, l2 = ks["k_wide_l1s"], ks["k_wide_last_ws"]
+    sq = sq_file("c3")
+    ex = c3.get("layer2_exact_f32", {})
+
+    def kern(d, inst):
+        out = {"kernel": inst, "ms": d["launch_ms"], "alg_bytes": d["alg_bytes_per_launch"],
+               "achieved_GBps": d["achieved_GBps"], "frac": d["frac"],
+               "frac_counter": d.get("frac_counter")}
+        s = sq.get(inst)
+        if s:
+            out["mfma_busy"] = s.get("mfma_busy")
+            out["wave_wait_frac"] = s.get("wait_frac")
+        return out
+
+    blk = {
+        "workload": f"c3 full graph (configs[2]): 1M nodes / 10M edges, 2-layer SAGE 128 + "
+                    f"Linear(128,1), every node a target, {c3['rows']} rows in 32-row passes",
+        "kernel": C3_DEFAULT_INSTANCES["k_wide_last_ws"],
+        "frac": l2["frac"], "achieved": l2["achieved_GBps"], "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac_counter": l2.get("frac_counter"),
+        "pass_ms": c3["pass_ms_rank0"],
+        "pass_frac": (l1["alg_bytes_per_launch"] + l2["alg_bytes_per_launch"]) /
+                     (c3["pass_ms_rank0"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "samples_per_s": c3["samples_per_s"],
+        "layer1": kern(l1, C3_DEFAULT_INSTANCES["k_wide_l1s"]),
+        "layer2": kern(l2, C3_DEFAULT_INSTANCES["k_wide_last_ws"]),
+    }
+    if ex:
+        blk["layer2_exact_f32"] = {"kernel": ex["kernel"], "ms": ex["layer2_ms"], "frac": ex["frac"],
+                                   "frac_counter": ex.get("frac_counter"),
+                                   "max_abs_diff_vs_bf16x3": ex.get("max_abs_diff_vs_bf16x3")}
+        s = sq.get(ex["kernel"])
+        if s:
+            blk["layer2_exact_f32"]["mfma_busy"] = s.get("mfma_busy")
+    # live MFMA rate of layer 2: per pass 32 samples x N targets x (K = 256) x (F_out = 128)
+    # products, each as three bf16 MFMA products (a_hi w_hi + a_hi w_lo + a_lo w_hi)
+    flops = 3 * 2.0 * 32 * 1_000_000 * 256 * 128
+    blk["mfma"] = {
+        "layer2_bf16_tflops": flops / (l2["launch_ms"] * 1e-3) / 1e12,
+        "peak_bf16_tflops": BF16_MFMA_PEAK_TF,
+        "rate_frac": flops / (l2["launch_ms"] * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF,
+        "busy": blk["layer2"].get("mfma_busy"),
+        "busy_clock_ghz": (sq.get(C3_DEFAULT_INSTANCES["k_wide_last_ws"]) or {}).get("clock_ghz"),
+        "busy_source": "profiles/sq_c3.json" if sq else None,
+        "note": "busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) of a "
+                "profiled run; rate_frac = the live layer-2 bf16 MFMA flops / 2.5 PF dense: the "
+                "kernel is HBM-gather-bound, MFMA is not its bound"}
+    return blk
+
+
+def compact_api(api):
+    """explainer_api with each phase as [host_ms, device_ms] (the bulky per-phase dicts kept the
+    driver's stdout tail from reaching the c3 section)."""
+    def ph(p):
+        if not isinstance(p, dict):
+            return p
+        return {k: [round(v.get("host_ms", 0.0), 3), round(v.get("device_ms") or 0.0, 3)]
+                if isinstance(v, dict) else round(v, 3) for k, v in p.items()}
+    out = {}
+    for k, v in api.items():
+        if isinstance(v, dict):
+            v = dict(v)
+            if "phases" in v:
+                v["phases_host_device_ms"] = ph(v.pop("phases"))
+            if isinstance(v.get("same_query_again"), dict):
+                a = dict(v["same_query_again"])
+                if "phases" in a:
+                    a["phases_host_device_ms"] = ph(a.pop("phases"))
+                v["same_query_again"] = a
+        out[k] = v
+    return out
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -1594,16 +1692,22 @@ def main():
     for key, name, fn in runners:
         if key in want:
             t0 = time.perf_counter()
-            log(rank, f"section {name} ...")
             regimes[name] = fn()
             torch.cuda.empty_cache()
-            log(rank, f"section {name} done in {time.perf_counter() - t0:.1f} s")
-    if regimes:
-        line["regimes"] = regimes
+            log(rank, f"section {name}: {time.perf_counter() - t0:.1f} s")
+    if "explainer_api" in regimes:
+        regimes["explainer_api"] = compact_api(regimes["explainer_api"])
+    if "c3_full_graph" in regimes and isinstance(line.get("roofline"), dict):
+        line["roofline"]["north_star"] = north_star_block(regimes["c3_full_graph"])
+    line["rank_layout"] = layout
     if skipped:
         line["sections_skipped"] = {"sections": list(skipped),
                                     "reason": f"single-GPU workloads (N = 1 only), not run at world {world}"}
-    line["rank_layout"] = layout
+    if regimes:
+        # the north-star section last: the end of the line is what a stdout tail keeps
+        order = [n for n in regimes if n != "c3_full_graph"] + \
+            (["c3_full_graph"] if "c3_full_graph" in regimes else [])
+        line["regimes"] = {n: regimes[n] for n in order}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

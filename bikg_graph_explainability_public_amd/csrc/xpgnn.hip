@@ -5332,8 +5332,13 @@ bool wide_overlap() {
   return !(e && std::strcmp(e, "0") == 0);
 }
 
-// one non-blocking side stream and the pass hand-off events per device, created once
+// one non-blocking side stream and the pass hand-off events per device, created once (the only
+// handles an entry point creates; no device memory).  `mu` is held across a call's whole enqueue
+// sequence: callers on different streams then never interleave their records of / waits on the
+// shared events (a wait binds to the record made before it, so a call's waits always see its own
+// records), and their side-stream work runs in call order.
 struct WideSide {
+  std::mutex mu;
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, l1[2] = {nullptr, nullptr}, l2[2] = {nullptr, nullptr};
 };
@@ -5527,8 +5532,10 @@ int run_wide_forward(const xpg_forward_plan* p, const WideWs& W, const uint32_t*
   XPG_HIP(hipStreamIsCapturing(st, &cap));
   WideSide* side = nullptr;
   const bool two = W.nset == 2 && cap == hipStreamCaptureStatusNone;
+  std::unique_lock<std::mutex> side_lock;
   if (two) {
     if (const int rc = wide_side(&side)) return rc;
+    side_lock = std::unique_lock<std::mutex>(side->mu);
     XPG_HIP(hipEventRecord(side->fork, st));
     XPG_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
   }

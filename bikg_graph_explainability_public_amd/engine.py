@@ -715,6 +715,7 @@ class ForwardPlan:
             self.n_out = 1
         self._upload_i32()
         self._ws = None
+        self._ws_stream = None  # raw handle of the stream that last used self._ws
 
     def _program_tensor(self, program, key, make):
         """Device tensors derived from the program's weights alone (padded biases, the stacked
@@ -764,7 +765,9 @@ class ForwardPlan:
         [rows, n_out] tensor to write y into (no allocation once the workspace exists).
         `workspace`: a uint8 device tensor of at least workspace_bytes(rows) to use instead of the
         plan's own — forwards running at the same time on different streams need one each (the
-        workspace holds the launch's block-scheduling counters)."""
+        workspace holds the launch's block-scheduling counters).  Without it, forwards on
+        different streams through one plan are ordered: each waits for the stream that used the
+        plan's workspace last."""
         _lib.require_device(bits, "bits")
         rows = bits.shape[0]
         if out is None:
@@ -792,6 +795,15 @@ class ForwardPlan:
         need = self.workspace_bytes(chunk)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        # the plan's own workspace (and the block counters in it) is reused in stream order: a
+        # forward on another stream than the last user's first waits for what that stream has
+        # queued (two streams forwarding through one plan then take turns instead of racing)
+        cur = st.value or 0  # 0: the null stream
+        if self._ws_stream is not None and self._ws_stream != cur and \
+                not torch.cuda.is_current_stream_capturing():
+            torch.cuda.current_stream(self.device).wait_stream(
+                torch.cuda.ExternalStream(self._ws_stream, device=self.device))
+        self._ws_stream = cur
         for r0 in range(0, rows, chunk):
             n = min(chunk, rows - r0)
             call("xpg_masked_forward", ctypes.byref(self.desc), ptr(bits[r0:r0 + n]), n,

@@ -127,4 +127,4 @@ def train_model(mask_loader, params, feat, edge_index, linear_model, arch, probl
 
 
 __all__ = ["LinearRegression", "model_updates", "regularizer", "train_model", "kernel_output",
-           "optimizer_scheduler", "weighted_mse_loss", "Data", "Model", "np"]
+           "optimizer_scheduler", "weighted_mse_loss", "Data", "Model"]

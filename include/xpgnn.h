@@ -4,9 +4,11 @@
  * Every entry point is `extern "C"`, takes plain device pointers + sizes + a HIP stream
  * (`xpg_stream_t`, NULL = legacy default stream) and returns an int status (XPG_OK = 0);
  * `xpg_last_error()` returns a thread-local message for the last failure.  No entry point
- * allocates, frees or synchronises (the xpg_profile_* measurement hooks aside): device memory
- * (inputs, outputs, workspaces) is owned by the caller (PyTorch tensors in the Python host), so
- * every call can be captured in a hipGraph.
+ * allocates device memory, frees or synchronises (the xpg_profile_* measurement hooks aside):
+ * device memory (inputs, outputs, workspaces) is owned by the caller (PyTorch tensors in the
+ * Python host), so every call can be captured in a hipGraph.  The one handle an entry point
+ * creates: xpg_masked_forward's wide path (more than one 32-row pass, stream not capturing)
+ * creates, once per device, a side stream and five events for its pass overlap.
  *
  * Mask bit layout ("row bits"): uint32 [rows][words], words = ceil(cols / 32); element c of
  * row r is bit (c & 31) of word r*words + (c >> 5).  Bits past `cols` in the last word are 0.
@@ -254,7 +256,9 @@ int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* by
  * mask row r (n_last = layers[n_layers-1].n_tgt; 1 for a single query); with edge_dot set,
  * y[r] = the decoded score of the target pair (dot_a, dot_b).  The workspace also holds the
  * launch's block-scheduling counters (zeroed on the stream before the kernel): calls that may
- * run at the same time (different streams) need workspaces of their own. */
+ * run at the same time (different streams) need workspaces of their own.  Concurrent calls from
+ * several host threads are safe under that rule: the wide path's shared side stream and pass
+ * events are held by one call's whole enqueue sequence at a time. */
 int xpg_masked_forward(const xpg_forward_plan* plan, const uint32_t* bits, int64_t rows,
                        float* y, void* workspace, size_t workspace_bytes, xpg_stream_t stream);
 

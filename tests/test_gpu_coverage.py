@@ -796,3 +796,78 @@ def test_h2d_staging_ring_uploads():
     for a, t in zip(arrays, outs):
         assert t.device == dev and t.shape == a.shape
         assert np.array_equal(t.cpu().numpy(), a)
+
+
+def _wide_plan(N=20_000, E=200_000, F=128, seed=4):
+    """A 2-layer SAGE 128 plan with every node a target: the wide path (>= 8192 targets)."""
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((N, F), generator=g)
+    ei = torch.randint(0, N, (2, E), generator=g)
+    torch.manual_seed(seed)
+    arch = ConvStack("sage", [F, F, F], [F, 1]).eval()
+    return pipeline.build_plan(arch.to(DEV), x.to(DEV), ei.to(DEV), list(range(N)))
+
+
+def test_wide_forward_two_threads_two_streams():
+    """The wide path's pass overlap shares one side stream and its hand-off events per device:
+    two host threads forwarding (96 rows = three 32-row passes, so both buffer sets and the
+    side stream are in use) on two streams with workspaces of their own must give the serial
+    outputs bit for bit (the enqueue sequence holds the side stream's lock)."""
+    import threading
+    e = _eng()
+    plan = _wide_plan()
+    N = plan.cols
+    bits = [e.sample_shapley(41 + i, 96, N, DEV) for i in range(2)]
+    ref = [plan.forward(b).clone() for b in bits]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=DEV) for _ in range(2)]
+    wss = [torch.empty(plan.workspace_bytes(96), dtype=torch.uint8, device=DEV) for _ in range(2)]
+    outs = [[torch.empty_like(ref[j]) for _ in range(4)] for j in range(2)]
+    errors = []
+    start = threading.Barrier(2)
+
+    def worker(j):
+        try:
+            start.wait()
+            with torch.cuda.stream(streams[j]):
+                for r in range(4):
+                    plan.forward(bits[j], out=outs[j][r], workspace=wss[j])
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append(ex)
+
+    th = [threading.Thread(target=worker, args=(j,)) for j in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for j in range(2):
+        for r in range(4):
+            assert torch.equal(outs[j][r], ref[j]), (j, r)
+
+
+def test_plan_workspace_ordered_across_streams():
+    """ForwardPlan.forward without `workspace=`: forwards through one plan issued on two streams
+    back to back (no host synchronisation) reuse the plan's workspace in stream order and give
+    the serial outputs (rows path: its block counters live in that workspace; wide path)."""
+    import argparse
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    e = _eng()
+    args = argparse.Namespace(nodes=100_000, edges=1_000_000, feat=64, query=7)
+    _, _, _, _, plan_rows = bench.build_c2(args, DEV)
+    for plan, R in ((plan_rows, 12800), (_wide_plan(), 96)):
+        bits = [e.sample_shapley(51 + i, R, plan.cols, DEV) for i in range(4)]
+        ref = [plan.forward(b).clone() for b in bits]
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream(device=DEV) for _ in range(2)]
+        outs = []
+        for i, b in enumerate(bits):
+            with torch.cuda.stream(streams[i % 2]):
+                outs.append(plan.forward(b))
+        torch.cuda.synchronize()
+        for i in range(4):
+            assert torch.equal(outs[i], ref[i]), i

@@ -59,6 +59,12 @@ for step in "$@"; do
            run pmc_fetch_c3 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 && \
            run pmc_write_c3 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 ;;
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
+    # c3 SQ + GRBM counters (MFMA busy, clock, wave waits) of the default and exact-f32 layer 2
+    sqc3) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+          run sq_c3_pass 300 bash tools/gpu/pmc_pass.sh sq_c3 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE GRBM_COUNT" "k_wide" python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 && \
+          python tools/sq_json.py gpurun_out/sq_c3 > gpurun_out/sq_c3.json ;;
+    # the tests this round added (wide two-thread / two-stream, workspace order, multi-rank c3)
+    newtests) run newtests 600 python -u -m pytest tests/test_gpu_coverage.py tests/test_gpu_multirank.py -m gpu -v -rf --timeout 300 --timeout-method thread -k "two_threads or workspace_ordered or multirank or rehearsal" ;;
     # k_agg_l1_rows ablations on the rows_ab plans (XPG_L1_DBG 1: no keep loads, 2: every source
     # the self row, 4: no output stores, or-ed; outputs invalid) + the kernel stats of the unablated run
     l1abl) for d in 0 1 2 3 4 7; do XPG_DIAGNOSTICS=1 XPG_L1_DBG=$d run l1abl_$d 200 python -u tools/rows_ab.py || exit 1; done && \
