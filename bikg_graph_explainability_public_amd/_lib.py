@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}
@@ -75,6 +75,8 @@ _SIGS = {
     "xpg_plan_arrays_take": ([c_vp, c_vp], c_i32),
     "xpg_plan_arrays_free": ([c_vp], c_i32),
     "xpg_mt19937_mask_bits": ([c_vp, c_vp, c_vp, c_i64, c_i64, c_vp], c_i32),
+    "xpg_mt19937_repeat_draws": ([c_vp, c_vp, c_vp, c_i32, c_i64, ctypes.c_float, ctypes.c_float, c_i32, c_vp,
+                                  c_vp], c_i32),
     "xpg_mt19937_community_bits": ([c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i64,
                                     c_vp], c_i32),
     "xpg_sample_communities": ([ctypes.c_uint64, c_i64, c_i64, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp,

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <cstring>
 #include <utility>
+#include <cmath>
 #include <vector>
 #if !defined(__HIP_DEVICE_COMPILE__)
 #include <emmintrin.h>  // SSE2 (x86-64 baseline): host code only
@@ -127,6 +128,37 @@ inline uint32_t next_u32(uint32_t* s, int32_t* left, int32_t* next) {
   y ^= (y << 15) & 0xefc60000u;
   y ^= y >> 18;
   return y;
+}
+
+// CPUGeneratorImpl::random64(): two outputs, the first one the high word
+inline uint64_t next_u64(uint32_t* s, int32_t* left, int32_t* next) {
+  const uint64_t hi = next_u32(s, left, next);
+  const uint64_t lo = next_u32(s, left, next);
+  return (hi << 32) | lo;
+}
+
+// The per-repeat draws of Explainer.run with the device Shapley sampler, in the reference's
+// order (explainer.py:490-519: mask_generator, LinearRegression init, DataLoader iterator), on
+// the CPU generator:
+//   seed  = torch.randint(0, 2**62, (1,))    uniform_int_from_to: random64() % 2^62
+//   w0[S] = torch.empty(S).uniform_(from, to) per element: x = (random() & (2^24 - 1)) * 2^-24 (float),
+//           x * (to - from) + from in float arithmetic (ATen uniform_real on dist_acctype<float>);
+//           `fma` = 1 evaluates it as one fused multiply-add (how a -mfma build of the ATen
+//           kernel may contract it; the CPU tests pin which form torch's build uses)
+//   base  = torch.empty((), int64).random_()  uniform_int<int64>: random64() % 2^63
+// seeds[times], w0[times][S]; the generator is left where torch would leave it.
+inline void repeat_draws(uint32_t* s, int32_t* left, int32_t* next, int times, int64_t S, float from, float to,
+                         int fma, int64_t* seeds, float* w0) {
+  const float span = to - from;
+  for (int t = 0; t < times; ++t) {
+    seeds[t] = static_cast<int64_t>(next_u64(s, left, next) % (1ULL << 62));
+    float* w = w0 + static_cast<int64_t>(t) * S;
+    for (int64_t i = 0; i < S; ++i) {
+      const float x = static_cast<float>(next_u32(s, left, next) & 0xFFFFFFu) * (1.0f / 16777216.0f);
+      w[i] = fma ? std::fma(x, span, from) : x * span + from;
+    }
+    (void)next_u64(s, left, next);  // the DataLoader's base seed (value unused)
+  }
 }
 
 // torch.randperm(n) on the CPU generator (ATen randperm_cpu, n < 2^32 / 20): Fisher-Yates with

@@ -5790,6 +5790,18 @@ int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t
   return XPG_OK;
 }
 
+int xpg_mt19937_repeat_draws(uint32_t* state, int32_t* left, int32_t* next, int32_t times, int64_t S, float from,
+                             float to, int32_t fma, int64_t* seeds, float* w0) {
+  XPG_REQ(state && left && next && times >= 0 && S >= 0 && (seeds || times == 0) && (w0 || times == 0 || S == 0) &&
+              from <= to,
+          "mt19937_repeat_draws: bad arguments");
+  const bool fresh = *left == 1 && *next == 0;
+  XPG_REQ(fresh || (*left >= 1 && *next >= 0 && *next + *left - 1 == hostrng::kN),
+          "mt19937_repeat_draws: generator position (left, next) is not an at::mt19937 state");
+  hostrng::repeat_draws(state, left, next, times, S, from, to, fma, seeds, w0);
+  return XPG_OK;
+}
+
 int xpg_mt19937_community_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t cols, int32_t n_comm,
                                const int32_t* comm_ptr, const int32_t* comm_cols, const int32_t* blocks,
                                int32_t n_blocks, int64_t rows, uint32_t* bits) {

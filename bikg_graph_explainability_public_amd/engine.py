@@ -119,6 +119,70 @@ def compat_shapley_bits(rows: int, cols: int):
     return out
 
 
+_DRAWS_FORM = []  # [form] once probed: 0 / 1 (see _draws_form), None = no native form matches
+
+
+def _draws_form():
+    """How this torch build evaluates ATen's CPU uniform_real, x * (to - from) + from in float:
+    as written (0) or contracted into one fused multiply-add (1) — the ATen kernels compiled for
+    an FMA-capable CPU capability contract it, the DEFAULT build does not.  Probed once on a
+    private generator (the global one is untouched) against both native forms; None when
+    neither reproduces torch (the caller then draws through torch itself)."""
+    if not _DRAWS_FORM:
+        form = None
+        g = torch.Generator().manual_seed(20260101)
+        st = g.get_state()
+        ref_seed = int(torch.randint(0, 2 ** 62, (1,), generator=g).item())
+        ref = torch.empty(1000).uniform_(-0.3, 0.3, generator=g)
+        torch.empty((), dtype=torch.int64).random_(generator=g)
+        ref_next = torch.rand(3, generator=g)
+        for f in (1, 0):
+            raw = st.numpy().copy()
+            left = raw[_RNG_LEFT:_RNG_LEFT + 4].view(np.int32).copy()
+            nxt = np.array([int(raw[_RNG_NEXT:_RNG_NEXT + 8].view(np.uint64)[0])], dtype=np.int32)
+            state = raw[_RNG_STATE:_RNG_STATE + 624 * 8].view(np.uint64).astype(np.uint32)
+            seeds = np.empty(1, dtype=np.int64)
+            w = torch.empty(1000)
+            call("xpg_mt19937_repeat_draws", state.ctypes.data, left.ctypes.data, nxt.ctypes.data, 1,
+                 1000, -0.3, 0.3, f, seeds.ctypes.data, w.data_ptr())
+            raw[_RNG_LEFT:_RNG_LEFT + 4] = left.view(np.uint8)
+            raw[_RNG_NEXT:_RNG_NEXT + 8] = np.array([nxt[0]], dtype=np.uint64).view(np.uint8)
+            raw[_RNG_STATE:_RNG_STATE + 624 * 8] = state.astype(np.uint64).view(np.uint8)
+            g2 = torch.Generator()
+            g2.set_state(torch.from_numpy(raw))
+            if int(seeds[0]) == ref_seed and torch.equal(w, ref) and \
+                    torch.equal(torch.rand(3, generator=g2), ref_next):
+                form = f
+                break
+        _DRAWS_FORM.append(form)
+    return _DRAWS_FORM[0]
+
+
+def repeat_draws(times: int, S: int, fma: int = None):
+    """Explainer.run's per-repeat draws on torch's global CPU generator with the device Shapley
+    sampler, in the reference's order (explainer.py:490-519), replayed natively
+    (xpg_mt19937_repeat_draws, host code): per repeat the sampler seed
+    torch.randint(0, 2**62, (1,)), LinearRegression(S)'s initial weights (wlm.py:40-45:
+    kaiming_uniform_(a=sqrt(5)) = uniform_(-bound, bound)) and the DataLoader iterator's seed
+    draw.  Returns (seeds: list of int, w0: float32 [times, S] host tensor); the generator is
+    left exactly where the torch calls leave it.  Returns None (nothing drawn) when this torch
+    build's uniform_ rounding matches neither native form (`_draws_form`)."""
+    from .wlm import LinearRegression
+    if fma is None:
+        fma = _draws_form()
+        if fma is None:
+            return None
+    bound = LinearRegression.init_bound(S)
+    seeds = np.empty(max(times, 1), dtype=np.int64)
+    w0 = torch.empty((times, S), dtype=torch.float32)
+    raw, state, left, nxt = _rng_get()
+    call("xpg_mt19937_repeat_draws", state.ctypes.data, left.ctypes.data, nxt.ctypes.data, int(times),
+         int(S), -bound, bound, int(fma), seeds.ctypes.data,
+         w0.data_ptr() if times and S else None)
+    _rng_set(raw, state, left, nxt)
+    return seeds[:times].tolist(), w0
+
+
 def compat_community_bits(cols: int, communities, blocks):
     """The reference's compat community draws (Mask.mask_generator with communities,
     masks.py:299-348 + pathways.py:234-385) on torch's global CPU generator, bit-identical, as
@@ -842,6 +906,27 @@ def check_fit_status(status):
             "surrogate fit: the multi-workgroup exchange timed out (workgroups not co-resident, "
             "e.g. another kernel or process held the GPU's CUs); the fitted weights are invalid. "
             "XPG_WLM=single selects the single-workgroup fit.")
+
+
+_STATUS_HOST = {}
+
+
+def status_to_host(status):
+    """Queue a copy of a fit's device status word into pinned host memory (no host wait) and
+    return the host tensor: once a later synchronising read on the stream (e.g. the results'
+    .cpu()) has returned, check_status_host(...) reads it without a second synchronisation."""
+    key = status.device.index
+    h = _STATUS_HOST.get(key)
+    if h is None:
+        h = _STATUS_HOST[key] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    h.copy_(status.reshape(-1)[:1], non_blocking=True)
+    return h
+
+
+def check_status_host(h):
+    """check_fit_status on a word copied by status_to_host (after the stream reached the copy)."""
+    if int(h[0]) != 0:
+        check_fit_status(torch.ones(1, dtype=torch.int32))
 
 
 WLM_KINDS = {0: "single", 1: "multi", 2: "grid"}

@@ -20,7 +20,7 @@ import weakref
 import numpy as np
 import torch
 
-from . import _lib, engine, pipeline, sharding
+from . import _lib, engine, frames, pipeline, sharding
 from .data import Data
 from .masks import Mask, dataloader_seed_draw
 from .model import Model
@@ -400,7 +400,16 @@ class Explainer:
             cplan = cmask.community_plan()
             ctabs = engine.community_tables(cplan, c["sub_pw_inds"], S, device)
         seeds = []  # device Shapley sampler: every repeat's seed first, then one native call
-        for _ in range(times):
+        draws = None
+        if on_device and c["sub_pw_inds"] is None:
+            # every repeat's seed, initial weights and DataLoader draw replayed natively from the
+            # generator state (the same numbers and end state as the torch calls below)
+            draws = engine.repeat_draws(times, S)
+        if draws is not None:
+            seeds = draws[0]
+            w0_list = draws[1]  # [times, S]: indexed per repeat like the list
+            masks = [None] * times
+        for _ in range(0 if draws is not None else times):
             if on_device and c["sub_pw_inds"] is None:
                 seeds.append(torch.randint(0, 2 ** 62, (1,)))  # read together below
                 masks.append(None)
@@ -417,7 +426,8 @@ class Explainer:
             w0_list.append(LinearRegression.initial_weights(S))
             dataloader_seed_draw()
         if seeds:
-            seeds = torch.cat(seeds).tolist()
+            if draws is None:
+                seeds = torch.cat(seeds).tolist()
             bits = engine.sample_shapley_sets(seeds, int(self.params["interpret_samples"] * epochs),
                                               S, device)       # [times, R, W]
         else:
@@ -430,12 +440,11 @@ class Explainer:
         flat = bits.reshape(times * R, -1)
         g = self.group
         sharding.assert_replicated(bits, "mask rows", g)
-        w0_all = torch.stack(w0_list)
+        w0_all = draws[1] if draws is not None else torch.stack(w0_list)
         sharding.assert_replicated(w0_all, "initial surrogate weights", g)
-        # the initial weights go to the device now, while the stream holds only the sampler: a
-        # pageable host -> device copy waits for the stream, so issued in the fit phase it held
-        # the host until the forward had finished and left the device idle while the fit launched
-        w0_dev = w0_all.to(device)
+        # the initial weights go to the device through the pinned staging ring (a pageable host ->
+        # device copy waits for everything queued on the stream first)
+        w0_dev = engine.h2d(w0_all.numpy(), device)
 
         clock.mark("plan")
 
@@ -531,6 +540,9 @@ class Explainer:
 
         fits = {}
         clock.mark("fit")
+        # the fits' exchange status is read with the results (one host synchronisation, in the
+        # output phase) instead of by a wait of its own right after the launch
+        status = torch.zeros(1, dtype=torch.int32, device=device)
 
         def fit(t0, t1):
             if t1 == t0:
@@ -540,7 +552,7 @@ class Explainer:
                 return torch.empty((0, S), device=device)
             w_, fits["losses"], fits["best"], _, _ = engine.wlm_fit(
                 bits[t0:t1], S, batch, y[t0:t1], kern[t0:t1], w0_dev[t0:t1],
-                self.params)
+                self.params, check=False, status=status)
             return w_
         w = sharding.gather_map(times, fit, g)
         losses = sharding.gather_rows(fits["losses"], times, g)
@@ -549,7 +561,20 @@ class Explainer:
                         kernel=kern, w0=w0_list)
         clock.mark("output")
         mean, std = self.weight_stacking(w)
-        config_val_df = Data(sub_feat, sub_ei).config_val_dataframe(mean, std, c["sub_names"])
+        status_h = engine.status_to_host(status)
+        # Data.config_val_dataframe (data.py:651-693); a computational subgraph's row labels are
+        # derived once per cached query (its names list is built by prepare() and belongs to the
+        # cache entry; the whole graph's columns are the caller's own names list, read each call)
+        labels = None
+        if c["pos"] is not None:
+            if "labels" not in c:
+                c["labels"] = frames.name_labels(c["sub_names"])
+            labels = c["labels"]
+        ms = torch.stack([mean.detach(), std.detach()]).cpu().numpy()
+        config_val_df = frames.sorted_frame(c["sub_names"], {"config_value_mean": ms[0],
+                                                             "config_value_std": ms[1]},
+                                            "config_value_mean", labels=labels)
+        engine.check_status_host(status_h)  # the frame's .cpu() waited for the copy
         pathway_df = None
         if c["has_pathways"]:
             pathway_df = Pathways(c["sub_pw"], c["sub_pw_names"]).aggregate(mean,

@@ -8,9 +8,18 @@ import numpy as np
 import pandas as pd
 
 
-def sorted_frame(names, columns, key, dropna=False):
+def name_labels(names):
+    """(labels, all_str): the row labels of `names` as an object array and whether pandas infers
+    them as strings — what sorted_frame derives from `names` on every call; a caller that builds
+    many frames over one unchanging names list computes it once and passes it in."""
+    labels = np.fromiter(names, dtype=object, count=len(names))
+    return labels, pd.api.types.infer_dtype(labels, skipna=False) == "string"
+
+
+def sorted_frame(names, columns, key, dropna=False, labels=None):
     """names: row labels (index "name"); columns: {column: 1-D array} in output order; rows
-    sorted by `key` descending; dropna drops every row with a NaN in any column."""
+    sorted by `key` descending; dropna drops every row with a NaN in any column.  `labels`:
+    name_labels(names), when the caller has it already."""
     cols = {c: np.asarray(v) for c, v in columns.items()}
     s = cols[key]
     nan = np.isnan(s) if s.dtype.kind == "f" else np.zeros(len(s), dtype=bool)
@@ -23,8 +32,8 @@ def sorted_frame(names, columns, key, dropna=False):
             if v.dtype.kind == "f":
                 bad |= np.isnan(v)
         order = order[~bad[order]]
-    labels = np.fromiter(names, dtype=object, count=len(names))
-    if pd.api.types.infer_dtype(labels, skipna=False) == "string":
+    labels, all_str = name_labels(names) if labels is None else labels
+    if all_str:
         # str labels: an object array skips pandas' per-element inference of a list (~0.2 ms at
         # 1.2k names); other label types keep the list constructor (int names -> int64 index)
         index = pd.Index(labels[order], name="name")

@@ -39,12 +39,16 @@ class LinearRegression(nn.Module):
         n = int(num_elements)
         if n == 0:
             return torch.empty(0)
-        # kaiming_uniform_(a=sqrt(5)) on [1, n]: fan_in n, leaky_relu gain, bound sqrt(3) * std
-        # (the same float operations, so the same bound and the same uniform_ draws)
-        gain = math.sqrt(2.0 / (1 + math.sqrt(5) ** 2))
-        bound = math.sqrt(3.0) * (gain / math.sqrt(n))
+        bound = LinearRegression.init_bound(n)
         with torch.no_grad():
             return torch.empty(n).uniform_(-bound, bound)
+
+    @staticmethod
+    def init_bound(n):
+        """kaiming_uniform_(a=sqrt(5)) on a [1, n] weight: fan_in n, leaky_relu gain, bound
+        sqrt(3) * std (the same float operations as torch.nn.init, so the same bound)."""
+        gain = math.sqrt(2.0 / (1 + math.sqrt(5) ** 2))
+        return math.sqrt(3.0) * (gain / math.sqrt(n))
 
 
 def model_updates(linear_model, loss, best_loss):

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 19
+#define XPG_ABI_VERSION 20
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -93,6 +93,14 @@ int xpg_sample_shapley_sets(const uint64_t* seeds, int32_t n_sets, int64_t rows,
  * torch.set_rng_state).  Bit-identical to the torch draw (v15). */
 int xpg_mt19937_mask_bits(uint32_t* state, int32_t* left, int32_t* next, int64_t rows, int64_t cols,
                           uint32_t* bits);
+/* HOST function (no GPU work): the per-repeat draws Explainer.run makes on torch's CPU generator
+ * with the device Shapley sampler, in the reference's order (explainer.py:490-519): per repeat
+ * the sampler seed torch.randint(0, 2**62, (1,)) -> seeds[t], the surrogate's initial weights
+ * LinearRegression(S) = uniform_(from, to) on S floats (wlm.py:40-45) -> w0[t][S], and the
+ * DataLoader iterator's base seed draw (value discarded).  State as in xpg_mt19937_mask_bits;
+ * `fma` selects the fused x * (to - from) + from form of ATen's uniform_real (v20). */
+int xpg_mt19937_repeat_draws(uint32_t* state, int32_t* left, int32_t* next, int32_t times, int64_t S,
+                             float from, float to, int32_t fma, int64_t* seeds, float* w0);
 /* HOST function (no GPU work): the reference's compat COMMUNITY draws (Mask.mask_generator with
  * communities, masks.py:299-348: per community in length-descending order get_internal_mask's
  * randint masks.py:130, Pathways.mask_generator's antithetic randint rows pathways.py:260-281,

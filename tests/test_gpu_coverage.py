@@ -871,3 +871,31 @@ def test_plan_workspace_ordered_across_streams():
         torch.cuda.synchronize()
         for i in range(4):
             assert torch.equal(outs[i], ref[i]), i
+
+
+def test_explainer_run_raises_on_fit_exchange_failure(monkeypatch):
+    """Explainer.run reads the fits' exchange status with the results (one synchronisation in
+    the output phase): a multi-workgroup fit whose partner never publishes (fault injection)
+    still makes run() raise FitExchangeError; the same call without the fault succeeds."""
+    from bikg_graph_explainability_public_amd import _lib
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    N = 2000
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn((N, 16), generator=g)
+    ei = torch.randint(0, N, (2, 8000), generator=g)
+    torch.manual_seed(0)
+    arch = ConvStack("gcn", [16, 16], [16, 1]).eval()
+    params = {"seed": 1, "interpret_samples": 24, "epochs": 10, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": "device"}
+    exp = Explainer(x.to(DEV), ei.to(DEV), arch, params, [str(i) for i in range(N)],
+                    problem="graph_prediction")
+    monkeypatch.setenv("XPG_WLM", "mc")
+    monkeypatch.setenv("XPG_DIAGNOSTICS", "1")
+    monkeypatch.setenv("XPG_MC_SPIN", "20000")
+    monkeypatch.setenv("XPG_MC_FAULT", "1")
+    with pytest.raises(_lib.FitExchangeError):
+        exp.run("7", 2)
+    monkeypatch.delenv("XPG_MC_FAULT")
+    df, _ = exp.run("7", 2)
+    assert len(df) == N and np.isfinite(df["config_value_mean"].to_numpy()).all()

@@ -50,6 +50,11 @@ for step in "$@"; do
     # 2 split poll, 3 both; alternating rounds on one box
     modes) for r in 1 2; do for md in 0 1 2 3; do XPG_MC_MODE=$md run probe_mode${md}_r$r 120 ./tools/wlm_probe 1193 12800 256; done; done ;;
     gw2) run gw2 300 ./tools/gw2_probe ;;
+    gprobe) run gather_probe 180 ./tools/gather_probe ;;
+    apitests) run apitests 600 python -u -m pytest tests -m gpu -q -rf --timeout 200 --timeout-method thread -k "explainer or golden or exchange or frame or query or Explainer" ;;
+    apisec) run api_sec 300 python bench.py --sections api --no-cpu-baseline ;;
+    apirep) run api_repeat 300 python -u tools/api_repeat.py && run api_repeat_nogc 300 python -u tools/api_repeat.py --no-gc && \
+            run api_repeat_c3 300 python -u tools/api_repeat.py --graph c3 ;;
     # layer-2 SQ counters (two PMC passes of <= 8 SQ counters) on one c3 pass of ws_ab.py
     wsprof) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
            run wssq1 300 bash tools/gpu/pmc_pass.sh sq1 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS" "k_wide_l1s|k_wide_last_ws" python3 tools/ws_ab.py --variants "${WSV:-B3=1}" --reps 1 && \
@@ -59,6 +64,10 @@ for step in "$@"; do
            run pmc_fetch_c3 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 && \
            run pmc_write_c3 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_c3 -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 ;;
     apiprof) run apiprof 300 python -u tools/api_profile.py ;;
+    # the API section alone, after the headline + c3 sections, and with cProfile of the repeated call
+    apictx) run api_alone 300 python bench.py --sections api --no-cpu-baseline && \
+            run api_after 400 python bench.py --sections headline,c3,api --no-cpu-baseline && \
+            XPG_BENCH_API_PROFILE=1 run api_prof 300 python bench.py --sections headline,c3,api --no-cpu-baseline ;;
     # c3 SQ + GRBM counters (MFMA busy, clock, wave waits) of the default and exact-f32 layer 2
     sqc3) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
           run sq_c3_pass 300 bash tools/gpu/pmc_pass.sh sq_c3 "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE GRBM_COUNT" "k_wide" python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --sections c3 && \
