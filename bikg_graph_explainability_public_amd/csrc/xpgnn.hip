@@ -5226,6 +5226,22 @@ int device_cus() {
   return cus;
 }
 
+// XCDs of the current device (hipDeviceAttributeNumberOfXccs: 8 on an MI355X in SPX mode, 1 per
+// device in CPX); 1 when the attribute is unavailable (the XCD-aware schedules then treat the
+// device as one XCD: correct, only without the per-XCD balance)
+int device_xcds() {
+  static int xcds = 0;
+  if (!xcds) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) == hipSuccess &&
+        n > 0 && n <= 8)
+      xcds = n;
+    else
+      xcds = 1;
+  }
+  return xcds;
+}
+
 // Optional per-kernel timing (xpg_profile_enable / xpg_profile_read): a pair of hipEvents on the
 // launch stream around each profiled launch, read back (and released) by xpg_profile_read.  Off
 // by default; never enable it around a graph capture.
@@ -5722,12 +5738,13 @@ int try_rows_forward(const xpg_forward_plan* p, const uint32_t* bits, int64_t ro
   }
   const size_t lds = sizeof(float) * (size_t)off;
   a.n_blocks = static_cast<int>(cdiv(rows, 64));
-  a.cus_per_xcd = std::max(1, device_cus() / 8);
+  a.cus_per_xcd = std::max(1, device_cus() / device_xcds());
   a.ctl = ctl;
   unsigned nwg = static_cast<unsigned>(a.n_blocks);
   if (ctl) {  // one workgroup per CU at most (LDS-bound); extra ones leave at once
     XPG_HIP(hipMemsetAsync(ctl, 0, sizeof(int) * 32, st));
-    nwg = static_cast<unsigned>(std::min<int64_t>(8 * a.cus_per_xcd, (int64_t)a.n_blocks + 4 * a.cus_per_xcd));
+    nwg = static_cast<unsigned>(std::min<int64_t>((int64_t)device_xcds() * a.cus_per_xcd,
+                                                  (int64_t)a.n_blocks + 4 * a.cus_per_xcd));
   }
   const dim3 grid(nwg);
 #define XPG_ROWS(F)                                                                                     \
@@ -6364,7 +6381,8 @@ static int wlm_layout(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch,
     const int64_t nrb = cdiv(batch, 64), ns = nrb <= 8 ? 1024 - 64 * nrb : 1024;
     // the staged rows / column vectors must fit kMcMaxStage words per stager: more parts if not
     while (P < kMcMaxP && std::max<int64_t>(batch, 32 * L->bw) * cdiv(words, P) > kMcMaxStage * ns) ++P;
-    while (P > 1 && (L->xcd ? cdiv(n_fits, 8) * P > device_cus() / 8 : n_fits * P > device_cus())) --P;
+    while (P > 1 && (L->xcd ? cdiv(n_fits, device_xcds()) * P > device_cus() / device_xcds() : n_fits * P > device_cus()))
+      --P;
     if (P >= 2) {
       const int wpp = static_cast<int>(cdiv(words, P));
       P = static_cast<int>(cdiv(words, wpp));

@@ -244,8 +244,14 @@ class Explainer:
         return True
 
     def clear_cache(self):
-        """Drop every cached query (computational subgraph, plan and its device buffers)."""
+        """Drop every cached query (computational subgraph, plan and its device buffers), the
+        architecture checks and the compiled programs with their padded weights.  The caches
+        are keyed on the inputs' storage and in-place version counters; an edit that bumps no
+        counter (through `param.data` or `tensor.data`, e.g. `p.data.copy_(w)`) is not seen by
+        them: call this after one."""
         self._queries.clear()
+        self._verified.clear()
+        pipeline.clear_programs()
 
     def _trim_cache(self, keep):
         """Keep the cache within params["plan_cache_bytes"] device bytes (default 2 GiB) and

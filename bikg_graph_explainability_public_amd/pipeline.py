@@ -35,6 +35,11 @@ def relation_edges(edge_index, edge_type, n_rel):
 _PROGRAMS = collections.OrderedDict()  # compiled_program's cache: key -> (weakref(arch), program)
 
 
+def clear_programs():
+    """Drop every cached compiled program and its padded device weights (compiled_program)."""
+    _PROGRAMS.clear()
+
+
 def compiled_program(arch, edge_type_names=None, node_type_names=None, state=None):
     """compile_arch(arch, ...) once per module state: keyed by the module (identity, checked by
     weak reference), every parameter and buffer (storage + in-place version counter: an
@@ -42,7 +47,9 @@ def compiled_program(arch, edge_type_names=None, node_type_names=None, state=Non
     The program carries the plans' weight-derived device tensors (ForwardPlan._program_tensor),
     so a new query's plan neither lowers the module nor re-pads its weights.  8 programs kept.
     `state`: the caller's (parameters, buffers) state tuples of this walk (Explainer.run reads
-    them once per call); None reads them here."""
+    them once per call); None reads them here.  An edit through `param.data` (e.g.
+    `p.data.copy_(w)`) bumps no version counter and is not seen: call clear_programs() (or
+    Explainer.clear_cache()) after one."""
     if state is None:
         state = (tuple((t.data_ptr(), t._version) for t in arch.parameters()),
                  tuple((t.data_ptr(), t._version) for t in arch.buffers()))

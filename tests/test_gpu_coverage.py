@@ -899,3 +899,31 @@ def test_explainer_run_raises_on_fit_exchange_failure(monkeypatch):
     monkeypatch.delenv("XPG_MC_FAULT")
     df, _ = exp.run("7", 2)
     assert len(df) == N and np.isfinite(df["config_value_mean"].to_numpy()).all()
+
+
+def test_explainer_clear_cache_sees_param_data_edits():
+    """An in-place edit through `param.data` bumps no version counter, so the query cache and the
+    compiled programs keep the old weights until Explainer.clear_cache(); after it, run() gives
+    what a fresh Explainer on the edited module gives."""
+    from bikg_graph_explainability_public_amd.explainer import Explainer
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    N = 3000
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn((N, 16), generator=g)
+    ei = torch.randint(0, N, (2, 12000), generator=g)
+    torch.manual_seed(2)
+    arch = ConvStack("gcn", [16, 16, 16], [16, 1]).eval()
+    params = {"seed": 1, "interpret_samples": 32, "epochs": 10, "optimizer": "adam", "lr": 0.01,
+              "lr_patience": 10, "l1_lambda": 1e-4, "mask_sampler": "compat"}
+    names = [str(i) for i in range(N)]
+    exp = Explainer(x.to(DEV), ei.to(DEV), arch, params, names)
+    exp.run("7", 1)
+    with torch.no_grad():
+        for p in arch.parameters():
+            p.data.mul_(-1.5)  # no version bump
+    exp.clear_cache()
+    df, _ = exp.run("7", 1)
+    fresh = Explainer(x.to(DEV), ei.to(DEV), arch, params, names)
+    df2, _ = fresh.run("7", 1)
+    np.testing.assert_allclose(df["config_value_mean"].to_numpy(),
+                               df2.loc[df.index, "config_value_mean"].to_numpy(), rtol=0, atol=1e-6)

@@ -98,8 +98,74 @@ def pipe2(fresh=False, graphs_n=2, ev_prod=True, ev_fin=True, ev_fit=True, unrol
     print(f"pipe2 (fresh={fresh} graphs={graphs_n} ev prod/fin/fit={ev_prod}/{ev_fin}/{ev_fit} u={unroll}): capture + replay ok, res[3][0] = {float(res[3][0])}", flush=True)
 
 
+def chain(kind):
+    """Minimal wait_stream constructs among side streams forked from the capture stream (round-6
+    bisection of the pipe2 segfault), each joined back before the capture ends:
+      wait_empty   B waits A, A has no work since the fork; B works
+      wait_chain   C waits B waits A, none of them worked yet; C works
+      seq3         A works; B waits A, works; C waits B, works
+      pingpong     A works; B waits A, works; A waits B, works
+      ring3x2      two rounds of: A waits C, works; B waits A, works; C waits B, works
+      ring3_first  ring3x2's first round only (A's first wait is on C before C worked)
+      ring3_late   like ring3x2 but A's first wait skipped (every wait follows work)"""
+    import torch
+    dev = torch.device("cuda", 0)
+    x = torch.ones(1 << 16, device=dev)
+    ss = [torch.cuda.Stream(device=dev) for _ in range(3)]
+    A, B, C = ss
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cur = torch.cuda.current_stream()
+        for st in ss:
+            st.wait_stream(cur)
+
+        def work(st, v):
+            with torch.cuda.stream(st):
+                x.add_(v)
+        if kind == "wait_empty":
+            B.wait_stream(A)
+            work(B, 1.0)
+        elif kind == "wait_chain":
+            B.wait_stream(A)
+            C.wait_stream(B)
+            work(C, 1.0)
+        elif kind == "seq3":
+            work(A, 1.0)
+            B.wait_stream(A)
+            work(B, 1.0)
+            C.wait_stream(B)
+            work(C, 1.0)
+        elif kind == "pingpong":
+            work(A, 1.0)
+            B.wait_stream(A)
+            work(B, 1.0)
+            A.wait_stream(B)
+            work(A, 1.0)
+        else:
+            rounds = 1 if kind == "ring3_first" else 2
+            for r in range(rounds):
+                if not (kind == "ring3_late" and r == 0):
+                    A.wait_stream(C)
+                work(A, 1.0)
+                B.wait_stream(A)
+                work(B, 1.0)
+                C.wait_stream(B)
+                work(C, 1.0)
+        for st in ss:
+            cur.wait_stream(st)
+    g.replay()
+    torch.cuda.synchronize()
+    print(f"{kind}: capture + replay ok, x[0] = {float(x[0])}", flush=True)
+
+
+CHAINS = ("wait_empty", "wait_chain", "seq3", "pingpong", "ring3_late", "ring3_first", "ring3x2")
+
+
 def child(variant):
     import torch
+    if variant in CHAINS:
+        return chain(variant)
     if variant in ("pipe2", "pipe2_fresh"):
         return pipe2(fresh=variant == "pipe2_fresh")
     if variant.startswith("p2:"):  # p2:g=1,prod=0,fin=1,fit=1,u=4

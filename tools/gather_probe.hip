@@ -49,6 +49,13 @@ __global__ __launch_bounds__(512) void rows(const float4* __restrict__ buf, int6
   if (acc == 1234.5f) out[0] = acc;
 }
 
+__global__ void fill(float4* p, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = mix(static_cast<uint32_t>(i));
+    p[i] = make_float4(h * 1e-9f, (h >> 3) * 1e-9f, (h >> 7) * 1e-9f, (h >> 11) * 1e-9f);
+  }
+}
+
 __global__ __launch_bounds__(512) void stream(const float4* __restrict__ p, int64_t n4, float* __restrict__ out) {
   float acc = 0.f;
   const int64_t stride = (int64_t)gridDim.x * 512;
@@ -73,7 +80,7 @@ int main() {
     printf("alloc failed\n");
     return 1;
   }
-  hipMemset(buf, 0, bytes);
+  fill<<<4096, 256>>>(buf, bytes / 16);  // random-looking values (a zero buffer can clock differently)
   hipDeviceSynchronize();
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);

@@ -25,6 +25,7 @@ for step in "$@"; do
     # both ranks on cuda:0 (the driver's 8-GPU runs use RCCL, one GPU per rank)
     rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
     capture) run capture 400 python tools/capture_probe.py ;;
+    capbisect) run capture_bisect 400 python tools/capture_probe.py wait_empty wait_chain seq3 pingpong ring3_late ring3_first ring3x2 "p2:g=1,prod=0,fin=0,fit=0,u=1" "p2:g=1,prod=0,fin=0,fit=0,u=2" ;;
     apitrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
               run apitrace 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d gpurun_out/apitrace -o run -- python3 tools/api_first_call_probe.py --queries 8,9,10 ;;
     htrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
@@ -53,6 +54,7 @@ for step in "$@"; do
     gprobe) run gather_probe 180 ./tools/gather_probe ;;
     apitests) run apitests 600 python -u -m pytest tests -m gpu -q -rf --timeout 200 --timeout-method thread -k "explainer or golden or exchange or frame or query or Explainer" ;;
     apisec) run api_sec 300 python bench.py --sections api --no-cpu-baseline ;;
+    covtests) run covtests 900 python -u -m pytest tests/test_gpu_coverage.py -m gpu -q -rf --timeout 300 --timeout-method thread ;;
     apirep) run api_repeat 300 python -u tools/api_repeat.py && run api_repeat_nogc 300 python -u tools/api_repeat.py --no-gc && \
             run api_repeat_c3 300 python -u tools/api_repeat.py --graph c3 ;;
     # layer-2 SQ counters (two PMC passes of <= 8 SQ counters) on one c3 pass of ws_ab.py
