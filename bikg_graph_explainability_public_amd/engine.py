@@ -52,22 +52,80 @@ def unpack_masks(bits: torch.Tensor, cols: int) -> torch.Tensor:
     return out.view(torch.bool)
 
 
+class CaptureTopologyError(RuntimeError):
+    """A stream dependency inside a HIP-graph capture that this HIP stack cannot end."""
+
+
 @contextlib.contextmanager
 def capture_guard():
     """Wrap every HIP-graph capture of the hot path (`with capture_guard(), torch.cuda.graph(g)`).
 
-    Freeing a captured graph while another capture runs aborts the process on this HIP stack
-    (tools/capture_probe.py, variant graph_gc, profiles/r3_capture_probe.log: the round-2
-    `capture_end` crash of the pipelined bench).  A graph object reachable only from a reference
-    cycle is freed whenever Python's cyclic collector runs, which can be mid-capture; the guard
-    collects first and holds the collector off until the capture ends.  The graphs themselves
-    must stay referenced by the caller (the bench keeps them in a list)."""
+    1. Freeing a captured graph while another capture runs aborts the process on this HIP stack
+       (tools/capture_probe.py, variant graph_gc, profiles/r3_capture_probe.log: the round-2
+       `capture_end` crash of the pipelined bench).  A graph object reachable only from a
+       reference cycle is freed whenever Python's cyclic collector runs, which can be
+       mid-capture; the guard collects first and holds the collector off until the capture
+       ends.  The graphs themselves must stay referenced by the caller.
+    2. Two side streams that wait on each other in turn segfault hipStreamEndCapture (minimal
+       construct, tools/capture_probe.py `pingpong`, profiles/r6_capture_bisect.log: A works;
+       B waits A, works; A waits B, works; all joined): the guard tracks the capture's stream
+       waits (Stream.wait_stream, Stream.wait_event on a recorded Event) and refuses a wait of
+       side stream X on side stream Y once Y has waited on X, with CaptureTopologyError, before
+       the wait is made; the side streams are joined to the capture's origin stream first, so
+       the capture still ends cleanly (and its graph is not used).  Waits between the origin
+       stream (the one current at the first wait) and a side stream are free in both
+       directions (the bench's pipelined lanes alternate them)."""
     gc.collect()
     enabled = gc.isenabled()
     gc.disable()
+    st = {"origin": None, "waited": {}, "streams": {}, "events": {}}
+    S, E = torch.cuda.Stream, torch.cuda.Event
+    orig_ws, orig_we, orig_rec = S.wait_stream, S.wait_event, E.record
+
+    def note(x, y):  # stream x is about to wait on stream y
+        if not torch.cuda.is_current_stream_capturing():
+            return
+        if st["origin"] is None:
+            cur = torch.cuda.current_stream()
+            st["origin"] = cur.cuda_stream
+            st["streams"][cur.cuda_stream] = cur
+        kx, ky = x.cuda_stream, y.cuda_stream
+        st["streams"].setdefault(kx, x)
+        st["streams"].setdefault(ky, y)
+        if kx == ky:
+            return
+        o = st["origin"]
+        if kx != o and ky != o and kx in st["waited"].get(ky, ()):
+            origin = st["streams"][o]
+            for k, s_ in st["streams"].items():
+                if k != o:
+                    orig_ws(origin, s_)
+            raise CaptureTopologyError(
+                "graph capture: side stream waits on a side stream that waited on it earlier in "
+                "the capture (A -> B -> A); hipStreamEndCapture segfaults on such a capture on "
+                "this HIP stack (tools/capture_probe.py pingpong).  Route the second wait through "
+                "the capture's origin stream.")
+        st["waited"].setdefault(kx, set()).add(ky)
+
+    def wait_stream(self, stream):
+        note(self, stream)
+        return orig_ws(self, stream)
+
+    def wait_event(self, event):
+        src = st["events"].get(id(event))
+        if src is not None:
+            note(self, src)
+        return orig_we(self, event)
+
+    def record(self, stream=None):
+        st["events"][id(self)] = stream if stream is not None else torch.cuda.current_stream()
+        return orig_rec(self, stream)
+
+    S.wait_stream, S.wait_event, E.record = wait_stream, wait_event, record
     try:
         yield
     finally:
+        S.wait_stream, S.wait_event, E.record = orig_ws, orig_we, orig_rec
         if enabled:
             gc.enable()
 

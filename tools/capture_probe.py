@@ -142,6 +142,29 @@ def chain(kind):
             work(B, 1.0)
             A.wait_stream(B)
             work(A, 1.0)
+        elif kind == "pingpong_cur":  # the same alternation with the capture stream itself
+            work(cur, 1.0)
+            A.wait_stream(cur)
+            work(A, 1.0)
+            cur.wait_stream(A)
+            work(cur, 1.0)
+        elif kind == "pingpong_nowork_b":  # B forwards A's dependency without work of its own
+            work(A, 1.0)
+            B.wait_stream(A)
+            A.wait_stream(B)
+            work(A, 1.0)
+        elif kind == "pingpong_end":  # A's second wait is its last operation
+            work(A, 1.0)
+            B.wait_stream(A)
+            work(B, 1.0)
+            A.wait_stream(B)
+        elif kind == "pingpong_join_first":  # B joined to cur before A waits on B
+            work(A, 1.0)
+            B.wait_stream(A)
+            work(B, 1.0)
+            cur.wait_stream(B)
+            A.wait_stream(cur)
+            work(A, 1.0)
         else:
             rounds = 1 if kind == "ring3_first" else 2
             for r in range(rounds):
@@ -159,7 +182,8 @@ def chain(kind):
     print(f"{kind}: capture + replay ok, x[0] = {float(x[0])}", flush=True)
 
 
-CHAINS = ("wait_empty", "wait_chain", "seq3", "pingpong", "ring3_late", "ring3_first", "ring3x2")
+CHAINS = ("wait_empty", "wait_chain", "seq3", "pingpong", "ring3_late", "ring3_first", "ring3x2",
+          "pingpong_cur", "pingpong_nowork_b", "pingpong_end", "pingpong_join_first")
 
 
 def child(variant):

@@ -26,6 +26,8 @@ for step in "$@"; do
     rank2) XPG_BENCH_BACKEND=gloo XPG_BENCH_ONE_GPU=1 run rank2 500 python bench.py --gpus 2 --sections headline,c3 --no-cpu-baseline --steps 20 ;;
     capture) run capture 400 python tools/capture_probe.py ;;
     capbisect) run capture_bisect 400 python tools/capture_probe.py wait_empty wait_chain seq3 pingpong ring3_late ring3_first ring3x2 "p2:g=1,prod=0,fin=0,fit=0,u=1" "p2:g=1,prod=0,fin=0,fit=0,u=2" ;;
+    capbisect2) run capture_bisect2 400 python tools/capture_probe.py pingpong_cur pingpong_join_first pingpong_nowork_b pingpong_end ;;
+    captests) run captests 200 python -u -m pytest tests/test_gpu_capture.py -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     apitrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
               run apitrace 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d gpurun_out/apitrace -o run -- python3 tools/api_first_call_probe.py --queries 8,9,10 ;;
     htrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
