@@ -27,6 +27,12 @@ for step in "$@"; do
     capture) run capture 400 python tools/capture_probe.py ;;
     capbisect) run capture_bisect 400 python tools/capture_probe.py wait_empty wait_chain seq3 pingpong ring3_late ring3_first ring3x2 "p2:g=1,prod=0,fin=0,fit=0,u=1" "p2:g=1,prod=0,fin=0,fit=0,u=2" ;;
     capbisect2) run capture_bisect2 400 python tools/capture_probe.py pingpong_cur pingpong_join_first pingpong_nowork_b pingpong_end ;;
+    # headline PMC passes on the grouped pipeline: --steps 6 --warmup 2 = groups of 2: 1 warm-up +
+    # 3 eager phase groups + 1 eager dev-seed group + 3 graph groups + 1 graph-check group = 9 ops
+    pmc_hl) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+           run pmc_fetch_headline 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_headline -o run -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --sections headline && \
+           run pmc_write_headline 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_headline -o run -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --sections headline ;;
+    hl3) for r in 1 2 3; do run hl_$r 200 python bench.py --sections headline,node_c3 --no-cpu-baseline; done ;;
     captests) run captests 200 python -u -m pytest tests/test_gpu_capture.py -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     apitrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
               run apitrace 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d gpurun_out/apitrace -o run -- python3 tools/api_first_call_probe.py --queries 8,9,10 ;;
