@@ -33,6 +33,8 @@ for step in "$@"; do
            run pmc_fetch_headline 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_fetch_headline -o run -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --sections headline && \
            run pmc_write_headline 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats --output-format csv -d gpurun_out/pmc_write_headline -o run -- python3 bench.py --steps 6 --warmup 2 --no-cpu-baseline --sections headline ;;
     hl3) for r in 1 2 3; do run hl_$r 200 python bench.py --sections headline,node_c3 --no-cpu-baseline; done ;;
+    wlmtests) run wlmtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_coverage.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wlm or run_queries or graph" ;;
+    gpsec) for r in 1 2; do run gp_$r 300 python bench.py --sections gp --no-cpu-baseline; done ;;
     captests) run captests 200 python -u -m pytest tests/test_gpu_capture.py -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     apitrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
               run apitrace 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d gpurun_out/apitrace -o run -- python3 tools/api_first_call_probe.py --queries 8,9,10 ;;

@@ -193,6 +193,90 @@ __global__ __launch_bounds__(WAVES * 64) void grad_kernel(const uint32_t* __rest
   }
 }
 
+// grad4: grad_kernel with the next row block prefetch optional and a waves-per-EU floor
+template <int WAVES, int MODE, bool PF, int MINW>
+__global__ __launch_bounds__(WAVES * 64, MINW) void grad4_kernel(const uint32_t* __restrict__ bits, int64_t rows,
+                                                          int64_t cols, int64_t words, int batch, int64_t t,
+                                                          const float* __restrict__ g, float* __restrict__ wg,
+                                                          float* __restrict__ mg, float* __restrict__ vg) {
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r0 = t * batch;
+  const int B = static_cast<int>((rows - r0) < batch ? (rows - r0) : batch);
+  const int ngrp = ((B + 31) / 32) * 8;
+  const int64_t w0 = (int64_t)blockIdx.x * kGwWords;
+  const int nw = static_cast<int>((words - w0) < kGwWords ? (words - w0) : kGwWords);
+  const uint32_t lmask = lane < nw ? ~0u : 0u;
+  const uint32_t wd = static_cast<uint32_t>(w0 + (lane < nw ? lane : 0));
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  uint32_t x[32];
+  if (wv * 32 < B) gw_load32<MODE>(bits, words, r0 + wv * 32, min(32, B - wv * 32), wd, x);
+  const int gp = ngrp | 1;
+  float* G = gsm;
+  float* colsum = gsm + ((16 * gp + 3) & ~3);
+  for (int grp = tid; grp < ngrp; grp += WAVES * 64) {
+    float a[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) a[b] = 4 * grp + b < B ? g[4 * grp + b] : 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      G[v * gp + grp] = ((v & 1) ? a[0] : 0.f) + ((v & 2) ? a[1] : 0.f) + ((v & 4) ? a[2] : 0.f) +
+                        ((v & 8) ? a[3] : 0.f);
+  }
+  for (int e = tid; e < 32 * 65; e += WAVES * 64) colsum[e] = 0.f;
+  __syncthreads();
+  float acc[32];
+#pragma unroll
+  for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+#pragma unroll 1
+  for (int rb = wv; rb * 32 < B; rb += WAVES) {
+    const int nr = min(32, B - rb * 32);
+    if (!PF && rb != wv) gw_load32<MODE>(bits, words, r0 + rb * 32, nr, wd, x);
+    uint32_t xn[32];
+    const int rbn = rb + WAVES;
+    if (PF && rbn * 32 < B) gw_load32<MODE>(bits, words, r0 + rbn * 32, min(32, B - rbn * 32), wd, xn);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) x[i] = i < nr ? (x[i] & lmask) : 0u;
+    transpose32(x);
+    const float* Gb = G + rb * 8;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      float s = 0.f;
+      if (MODE == 1) {
+        s = __uint_as_float((x[b] & 0x007FFFFFu) | 0x3F800000u);
+      } else {
+#pragma unroll
+        for (int n = 0; n < 8; ++n) s += Gb[((x[b] >> (4 * n)) & 15u) * gp + n];
+      }
+      acc[b] += s;
+    }
+    if (PF) {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) x[k] = xn[k];
+    }
+  }
+  for (int w = 0; w < WAVES; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int b = 0; b < 32; ++b) colsum[b * 65 + lane] += acc[b];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < 32 * kGwWords; e += WAVES * 64) {
+    const int64_t c = w0 * 32 + e;
+    if (c < cols) {
+      const float gsum = colsum[(e & 31) * 65 + (e >> 5)];
+      float w = wg[c], m = mg[c], v = vg[c];
+      m = fmaf(0.1f, gsum - m, m);
+      v = fmaf(0.001f, gsum * gsum, v * 0.999f);
+      w = w - 0.01f * (m / (sqrtf(v) + 1e-8f));
+      wg[c] = w;
+      mg[c] = m;
+      vg[c] = v;
+    }
+  }
+}
+
 // v2 candidates: the lookups of two rows (16 table reads) issued before any of them is summed,
 // the rows of the batch split over gridDim.y workgroups (balanced grids), 16 lookups per round
 template <int WAVES, int MODE>
@@ -637,6 +721,14 @@ int main() {
   });
   P(8, 0) P(8, 1) P(8, 2) P(4, 0) P(16, 0)
   G(4, 0) G(4, 1) G(4, 2) G(8, 0) G(16, 0)
+#define G4(WV, PF, MINW)                                                                                  \
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&grad4_kernel<WV, 0, PF, MINW>),                       \
+                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_g));                \
+  timeit("grad4<" #WV ",pf" #PF ",minw" #MINW ">", [&](int t) {                                             \
+    hipLaunchKernelGGL((grad4_kernel<WV, 0, PF, MINW>), dim3(n_wg), dim3(WV * 64), lds_g, 0, bits, rows, cols, \
+                       words, B, t, g, w, m, v);                                                           \
+  });
+  G4(4, true, 1) G4(4, false, 4) G4(4, true, 4) G4(8, false, 4) G4(8, true, 4) G4(8, false, 2) G4(16, false, 4)
 #define P2(WV, MD, SPLIT)                                                                                  \
   timeit("p2<" #WV "," #MD "> x" #SPLIT, [&](int t) {                                                      \
     hipLaunchKernelGGL((p2_kernel<WV, MD>), dim3(n_wg, SPLIT), dim3(WV * 64), 0, 0, bits, rows, cols, words, B, \
