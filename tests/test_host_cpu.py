@@ -588,3 +588,46 @@ def test_community_filtering_drops_empty_communities():
     exp, z, meta = build_explainer("test_run")
     ctx = exp.prepare(meta["element"], torch.device("cpu"))
     assert all(len(c) > 0 for c in ctx["sub_pw_inds"])
+
+
+@pytest.mark.parametrize("level", ["sse2", "avx2", "avx512", "native"])
+def test_compat_replay_every_simd_path(level):
+    """The native mt19937 replay's SIMD paths (XPG_HOST_SIMD caps the level: SSE2 baseline, AVX2,
+    AVX-512, AVX-512 + VPOPCNTDQ where the CPU has them) all give torch's bool draw bit for bit,
+    from generator positions across state regenerations, and leave the generator where torch
+    does (each level in its own process: the level is read once)."""
+    import subprocess
+    import sys
+    code = r"""
+import numpy as np, torch, oracle
+from bikg_graph_explainability_public_amd import engine, _lib
+_lib.load()
+for seed, skip, rows, cols in [(1, 0, 300, 1193), (2, 623, 77, 40), (3, 311, 129, 33), (4, 1, 64, 1024), (5, 5000, 31, 997)]:
+    torch.manual_seed(seed)
+    torch.empty(skip).uniform_()
+    st = torch.get_rng_state()
+    ref = torch.randint(0, 2, (rows, cols), dtype=torch.bool); after = torch.rand(4)
+    torch.set_rng_state(st)
+    b = engine.compat_shapley_bits(rows, cols); after2 = torch.rand(4)
+    assert np.array_equal(b.numpy().view(np.uint32), oracle.pack_bits(ref.numpy())), (seed, skip)
+    assert torch.equal(after, after2), (seed, skip)
+    torch.set_rng_state(st)
+    s1, w1 = engine.repeat_draws(3, cols)
+    torch.set_rng_state(st)
+    s2 = []; w2 = []
+    for _ in range(3):
+        s2.append(int(torch.randint(0, 2 ** 62, (1,)).item()))
+        from bikg_graph_explainability_public_amd.wlm import LinearRegression
+        w2.append(LinearRegression.initial_weights(cols))
+        torch.empty((), dtype=torch.int64).random_()
+    assert s1 == s2 and torch.equal(w1, torch.stack(w2)), (seed, skip)
+print("ok")
+"""
+    env = dict(os.environ)
+    if level != "native":
+        env["XPG_HOST_SIMD"] = level
+    else:
+        env.pop("XPG_HOST_SIMD", None)
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-3000:]
