@@ -35,6 +35,7 @@ for step in "$@"; do
     hl3) for r in 1 2 3; do run hl_$r 200 python bench.py --sections headline,node_c3 --no-cpu-baseline; done ;;
     wlmtests) run wlmtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_coverage.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wlm or run_queries or graph" ;;
     gpsec) for r in 1 2; do run gp_$r 300 python bench.py --sections gp --no-cpu-baseline; done ;;
+    early2) run early2 500 python -u tools/ws_ab.py --rows 64 --reps 3 --variants "OVERLAP=0;OVERLAP=0,EARLY2=1;OVERLAP=0;OVERLAP=0,EARLY2=1;OVERLAP=1;OVERLAP=1,EARLY2=1" ;;
     captests) run captests 200 python -u -m pytest tests/test_gpu_capture.py -m gpu -v -rf --timeout 120 --timeout-method thread ;;
     apitrace) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
               run apitrace 300 rocprofv3 --kernel-trace --hip-trace --memory-copy-trace --output-format csv -d gpurun_out/apitrace -o run -- python3 tools/api_first_call_probe.py --queries 8,9,10 ;;
