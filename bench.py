@@ -339,8 +339,8 @@ def headline(args, dev, world, rank, workload="c2"):
     """The repeat pipeline of a node_prediction workload (c2: the headline; c3node: regime (i)
     of configs[2]), sharded as Explainer.run shards it (module docstring).
 
-    A step is one repeat (its own masks, forward, KernelSHAP and surrogate fit).  With one rank
-    the pipelined graphs take the steps in groups of G (XPG_BENCH_GROUP, default 2; 1 = the
+    A step is one repeat per rank (its own masks, forward, KernelSHAP and surrogate fit).  The
+    pipelined graphs take each rank's steps in groups of G (XPG_BENCH_GROUP, default 2; 1 = the
     round-5 form): the G repeats' masks -> forward -> KernelSHAP run as one production and
     their G fits as ONE k_wlm_fit_mc launch, which places each fit on its own XCD, so the G
     latency-bound fits run side by side (as Explainer.run(times) batches its repeats).  The
@@ -349,8 +349,7 @@ def headline(args, dev, world, rank, workload="c2"):
     78-80 M samples/s, groups of 2 135 M, of 4 181 M).  Every one of the K steps is still
     processed in full inside the timed region; the line reports K steps of one repeat each."""
     group = 1
-    if world == 1 and args.repeats == 1 and not args.no_graph and \
-            os.environ.get("XPG_BENCH_PIPE", "1") == "1":
+    if args.repeats == 1 and not args.no_graph and os.environ.get("XPG_BENCH_PIPE", "1") == "1":
         g = max(1, int(os.environ.get("XPG_BENCH_GROUP", "2")))
         if g > 1 and args.steps % g == 0:
             group = g
@@ -362,7 +361,7 @@ def headline(args, dev, world, rank, workload="c2"):
     line["steps"], line["warmup"] = args.steps, args.warmup
     line["ms_per_step"] = line["ms_per_step"] / group
     cfg = line["config"]
-    cfg["repeats_per_step"] = 1
+    cfg["repeats_per_step"] = world  # one repeat per rank per step
     cfg["steps_per_group"] = group
     cfg["fits_in_flight"] = group
     cfg["launch"] = (f"pipelined captured HIP graphs over groups of {group} consecutive steps "
