@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxpgnn.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 MAX_TERMS = 8
 
 ACT = {None: 0, "identity": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leaky_relu": 4, "elu": 5}

@@ -4721,6 +4721,32 @@ __device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lan
   return v[0] + __shfl_xor(v[0], 1);
 }
 
+// Sum of v[0..7] over the wave's 64 lanes for every i: after the call lanes 8i..8i+7 hold
+// sum_lanes v[i] (3 halving exchange stages, then 3 butterfly stages over the 8-lane groups).
+__device__ __forceinline__ float wave_transpose_reduce8(float (&v)[8], int lane) {
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {
+    const int half = 4 >> st;
+    const int xm = 32 >> st;
+    const bool hi = (lane & xm) != 0;
+#pragma unroll
+    for (int k = 0; k < half; ++k) {
+      float lo_v = v[k], hi_v = v[k + half];
+      asm volatile("" : "+v"(lo_v), "+v"(hi_v));
+      const float keep = hi ? hi_v : lo_v;
+      const float send = hi ? lo_v : hi_v;
+      float r = keep + __shfl_xor(send, xm);
+      asm volatile("" : "+v"(r));
+      v[k] = r;
+    }
+  }
+  float r = v[0];
+  r += __shfl_xor(r, 4);
+  r += __shfl_xor(r, 2);
+  r += __shfl_xor(r, 1);
+  return r;
+}
+
 // x[i] = word `wd` of row row0 + i for i < nr, else 0.  row0 / nr are wave-uniform, so the row
 // test is a scalar branch and all loads are in flight together (no per-lane exec masking);
 // callers mask lanes past the chunk.
@@ -4943,6 +4969,335 @@ __global__ __launch_bounds__(64) void k_gw_loss(const double* __restrict__ tk_pa
               static_cast<double>(reg);
 }
 
+
+// ------------------------------------------------------------ surrogate, fused many-column fit
+// The three launches per Adam step above read the step's mask bits twice from HBM (p, then the
+// gradient) and stream w / m / v (24 B per column) through HBM every step.  k_gw_fused is ONE
+// persistent launch per fit: nwg co-resident 512-thread workgroups (one per CU, LDS-bound), each
+// owning `ch` chunks of 64 mask words (2048 columns).  Per step:
+//   phase 1  the step's bits of the own chunks are in registers (x[4][32]: a wave holds four
+//            32-row blocks of one chunk, lane = word; 8 waves at up to 256 VGPRs); p partials by
+//            the nibble tables of w (as k_gw_p), chunk partials added in chunk order, published
+//            as tagged 8-B granules {step + 1, p} -> xp[row][wg]
+//   reduce   row j belongs to workgroup j mod nwg: one wave polls its nwg granules, sums them
+//            (lane-strided, then a fixed butterfly), g_j = k_j cg (p_j - ybar), p_hist, the loss
+//            term; publishes {step + 1, g_j} -> xg[j]
+//   phase 3  every workgroup polls the batch's g, builds 4-row G tables, and the SAME bit
+//            registers (transposed in place) give the column sums (as k_gw_grad); the waves of a
+//            chunk add their sums in a fixed tree through LDS; Adam on w / m / v held in LDS for
+//            the whole fit; the next step's bits are loaded into the freed registers right after
+//            the lookups, in flight during the tree, Adam and the w-table build
+// so a step reads its bits once and w / m / v never leave the CU until the end.  Granule slots
+// are cleared by k_wlm_stats before the launch (tags t + 1 never match a cleared slot); data
+// flow makes one slot per row enough (a row's step-(t+1) granule is written only after every
+// workgroup read the step-t g values, i.e. after every reducer finished step t).  Polls are
+// bounded: a workgroup that never arrives sets the error word, every workgroup leaves, and the
+// caller's status word reports it (k_argmin_first).  All arithmetic is deterministic.
+constexpr int kGfMaxCh = 2;        // chunks per workgroup (LDS: w tables + w / m / v per chunk)
+constexpr int kGfWaves = 8;        // waves per workgroup
+constexpr int kGfTpw = 4;          // resident 32-row blocks per wave
+constexpr int kGfThreads = kGfWaves * 64;
+constexpr int kGfColPitch = 65;    // column-sum image [b][j] pitch: conflict-free both ways
+
+struct GfArgs {
+  const uint32_t* bits;
+  const double* kern;
+  const WlmStep* stp;
+  float *wg, *mg, *vg, *p_hist;
+  double *tk_part, *aw_part;  // [steps][nwg]
+  uint64_t* xp;               // [batch][nwg] p granules, then [batch] g granules
+  uint32_t* err;
+  xpg_wlm_params P;
+  int rows, cols, words, steps, batch, ch, nrbp, nwg, fault_wg;
+  uint32_t spin_limit;
+};
+
+// LDS image of k_gw_fused (floats): [R0: w tables | tree slots][cs][w][m][v][pp][gb][G] + doubles.
+// nrbp = row blocks rounded up to kGfTpw; a chunk has nrbp / kGfTpw waves.
+struct GfLds {
+  int r0, cs, w, m, v, pp, gb, G, gp, slots, total;  // float offsets; total in floats (doubles follow)
+};
+__host__ __device__ inline GfLds gf_lds(int ch, int nrbp) {
+  GfLds L;
+  const int nwc = nrbp / kGfTpw, slots = nwc / 2 > 4 ? nwc / 2 : 4;
+  L.gp = (nrbp * 8) | 1;
+  L.slots = slots;
+  int o = 0;
+  L.r0 = o;  o += ch * slots * 2048;  // >= ch * 8 * 16 * 64 (the w tables)
+  L.cs = o;  o += ch * 32 * kGfColPitch;
+  L.w = o;   o += ch * 2048;
+  L.m = o;   o += ch * 2048;
+  L.v = o;   o += ch * 2048;
+  L.pp = o;  o += ch * nrbp * 32;
+  L.gb = o;  o += nrbp * 32;
+  L.G = o;   o += 16 * L.gp;
+  L.total = (o + 1) & ~1;
+  return L;
+}
+
+__device__ __forceinline__ float gf_poll(const uint64_t* p, uint32_t tag, uint32_t spin_limit, uint32_t* err,
+                                         int* abort_s) {
+  uint64_t v = ld64_sc1(p);
+  uint32_t n = 0;
+  while (static_cast<uint32_t>(v >> 32) != tag) {
+    __builtin_amdgcn_s_sleep(1);
+    v = ld64_sc1(p);
+    ++n;
+    if (n > spin_limit || ((n & 63u) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *abort_s = 1;
+      return 0.f;
+    }
+  }
+  return __uint_as_float(static_cast<uint32_t>(v));
+}
+
+__global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform roles and row blocks
+  const int wg = blockIdx.x, CH = a.ch, nwc = a.nrbp / kGfTpw;
+  const GfLds L = gf_lds(CH, a.nrbp);
+  double* red = reinterpret_cast<double*>(gsm + L.total);  // [kGfWaves] aw, [kGfWaves] tk
+  __shared__ int abort_s;
+  if (tid == 0) abort_s = 0;
+  const int n_chunks = (a.words + kGwWords - 1) / kGwWords;
+  const int chunk0 = wg * CH;
+  const int nch = min(CH, n_chunks - chunk0);  // own chunks (>= 1)
+  // this wave's role in phases 1 / 3: chunk h, row blocks kGfTpw * k ...
+  const int h = wave / nwc, k = wave - h * nwc;
+  const bool wvalid = h < nch;
+  const int w0 = (chunk0 + (wvalid ? h : 0)) * kGwWords;
+  const int nw = min(kGwWords, a.words - w0);
+  const uint32_t lmask = lane < nw ? ~0u : 0u;
+  const uint32_t wd = static_cast<uint32_t>(w0 + (lane < nw ? lane : 0));
+  const int64_t c_lo = (int64_t)chunk0 * 2048;  // first own column
+  float* Wt = gsm + L.r0;
+  float* cs = gsm + L.cs;
+  float* Wv = gsm + L.w;
+  float* Mv = gsm + L.m;
+  float* Vv = gsm + L.v;
+  float* pp = gsm + L.pp;
+  float* gb = gsm + L.gb;
+  float* G = gsm + L.G;
+  const int gp = L.gp;
+  const int RB = a.nrbp * 32;
+  const uint32_t pitch = static_cast<uint32_t>(a.words) * 4u;
+
+  uint32_t x[kGfTpw][32];
+  // the bits of step t's row block kGfTpw * k + u: buffer loads (descriptor at the block's first
+  // row in SGPRs, lane word in voffset, row in soffset); rows past the batch re-read its last row
+  // (masked at use)
+  auto load_block = [&](int64_t t, int u) {
+    const int64_t r0 = t * a.batch;
+    const int B = static_cast<int>(min((int64_t)a.batch, (int64_t)a.rows - r0));
+    const int rb = kGfTpw * k + u;
+    if (wvalid && rb * 32 < B) {
+      const int last = min(32, B - rb * 32) - 1;
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint32_t*>(a.bits + (r0 + rb * 32) * (int64_t)a.words), 0,
+          static_cast<int>(pitch * static_cast<uint32_t>(last + 1)), 0x00020000);
+#pragma unroll
+      for (int i = 0; i < 32; ++i)
+        x[u][i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wd * 4u, static_cast<uint32_t>(min(i, last)) * pitch, 0);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < kGfTpw; ++u) load_block(0, u);  // in flight during the set-up
+
+  // w / m / v of the own columns into LDS (0 past cols), then the w tables
+  for (int e = tid; e < CH * 2048; e += kGfThreads) {
+    const int64_t c = c_lo + e;
+    const bool ok = (e >> 11) < nch && c < a.cols;
+    Wv[e] = ok ? a.wg[c] : 0.f;
+    Mv[e] = ok ? a.mg[c] : 0.f;
+    Vv[e] = ok ? a.vg[c] : 0.f;
+  }
+  auto build_w_tables = [&]() {
+    for (int task = tid; task < CH * 8 * 64; task += kGfThreads) {
+      const int hh = task >> 9, q = (task >> 6) & 7, j = task & 63;
+      const float* wq = Wv + hh * 2048 + 32 * j + 4 * q;
+      const float a0 = wq[0], a1 = wq[1], a2 = wq[2], a3 = wq[3];
+      float* Tq = Wt + ((hh * 8 + q) * 16) * 64 + j;
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        Tq[v * 64] = ((v & 1) ? a0 : 0.f) + ((v & 2) ? a1 : 0.f) + ((v & 4) ? a2 : 0.f) + ((v & 8) ? a3 : 0.f);
+    }
+  };
+  lds_barrier();
+  build_w_tables();
+  lds_barrier();
+
+  const float l1s = a.P.l1_lambda / static_cast<float>(a.cols);
+  bool aborted = false;
+  for (int t = 0; t < a.steps; ++t) {
+    const WlmStep sc = a.stp[t];
+    const int64_t r0 = (int64_t)t * a.batch;
+    const int B = static_cast<int>(min((int64_t)a.batch, (int64_t)a.rows - r0));
+    const uint32_t tag = static_cast<uint32_t>(t + 1);
+    // ---- phase 1: chunk partials of p over the own words, 8 rows at a time
+    if (wvalid) {
+      const float* Tl = Wt + h * 8 * 16 * 64 + lane;
+#pragma unroll
+      for (int u = 0; u < kGfTpw; ++u) {
+        const int rb = kGfTpw * k + u;
+        const int nr = min(32, B - rb * 32);
+        if (nr > 0) {
+#pragma unroll
+          for (int i0 = 0; i0 < 32; i0 += 8) {
+            float c[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const uint32_t xi = i0 + i < nr ? (x[u][i0 + i] & lmask) : 0u;
+              float s = 0.f;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) s += Tl[(q * 16 + ((xi >> (4 * q)) & 15u)) * 64];
+              c[i] = s;
+            }
+            const float tot = wave_transpose_reduce8(c, lane);  // row i0 + (lane >> 3)
+            const int i = i0 + (lane >> 3);
+            if (!(lane & 7) && i < nr) pp[h * RB + rb * 32 + i] = tot;
+          }
+        }
+      }
+    }
+    lds_barrier();
+    // ---- publish the workgroup's partial of every row (chunks added in order)
+    if (!(a.fault_wg == wg && t == 0)) {
+      for (int r = tid; r < B; r += kGfThreads) {
+        float v = 0.f;
+        for (int hh = 0; hh < nch; ++hh) v += pp[hh * RB + r];
+        st64_sc1(a.xp + (int64_t)r * a.nwg + wg, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(v));
+      }
+    }
+    // ---- reduce the rows this workgroup owns: p_j, g_j, the loss term
+    double tk = 0.0;
+    for (int j = wg + wave * a.nwg; j < B; j += kGfWaves * a.nwg) {
+      const uint64_t* src = a.xp + (int64_t)j * a.nwg;
+      float part = 0.f;
+      for (int c = lane; c < a.nwg; c += 64) part += gf_poll(src + c, tag, a.spin_limit, a.err, &abort_s);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+      const float p = __shfl(part, 0);
+      if (lane == 0) {
+        const double kj = a.kern[r0 + j];
+        const double d = static_cast<double>(p) - sc.ybar;
+        const float g = static_cast<float>(kj * sc.cg * d);
+        a.p_hist[r0 + j] = p;
+        tk += kj * d * d;
+        st64_sc1(a.xp + (int64_t)a.batch * a.nwg + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(g));
+      }
+    }
+    if (lane == 0) red[kGfWaves + wave] = tk;
+    // ---- the batch's g (rows past B: 0)
+    for (int r = tid; r < RB; r += kGfThreads)
+      gb[r] = r < B ? gf_poll(a.xp + (int64_t)a.batch * a.nwg + r, tag, a.spin_limit, a.err, &abort_s) : 0.f;
+    lds_barrier();
+    if (abort_s) {
+      aborted = true;
+      break;
+    }
+    if (tid == 0) {
+      double s = 0.0;
+      for (int i = 0; i < kGfWaves; ++i) s += red[kGfWaves + i];
+      a.tk_part[(int64_t)t * a.nwg + wg] = s;
+    }
+    for (int e = tid; e < 16 * (a.nrbp * 8); e += kGfThreads) {  // G[v * gp + group]
+      const int v = e / (a.nrbp * 8), grp = e - v * (a.nrbp * 8);
+      const float* gg = gb + 4 * grp;
+      G[v * gp + grp] = ((v & 1) ? gg[0] : 0.f) + ((v & 2) ? gg[1] : 0.f) + ((v & 4) ? gg[2] : 0.f) +
+                        ((v & 8) ? gg[3] : 0.f);
+    }
+    lds_barrier();
+    // ---- phase 3: column sums from the same registers; each block's registers take the next
+    // step's bits as soon as its lookups are done
+    float acc[32];
+#pragma unroll
+    for (int b = 0; b < 32; ++b) acc[b] = 0.f;
+#pragma unroll
+    for (int u = 0; u < kGfTpw; ++u) {
+      const int rb = kGfTpw * k + u;
+      const int nr = min(32, B - rb * 32);
+      if (wvalid && nr > 0) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) x[u][i] = i < nr ? (x[u][i] & lmask) : 0u;
+        transpose32(x[u]);  // x[u][b] = column 32 * word + b over the block's rows
+        const float* Gb = G + rb * 8;
+#pragma unroll
+        for (int b = 0; b < 32; ++b) {
+          float s = 0.f;
+#pragma unroll
+          for (int n = 0; n < 8; ++n) s += Gb[((x[u][b] >> (4 * n)) & 15u) * gp + n];
+          acc[b] += s;
+        }
+      }
+      if (t + 1 < a.steps) load_block(t + 1, u);
+    }
+    // the chunk's waves add their column sums in a fixed tree (wave k += wave k + m)
+    for (int n = nwc; n > 1;) {
+      const int m = (n + 1) >> 1;
+      float* slot = Wt + h * L.slots * 2048;  // this chunk's slots (over its w tables)
+      if (wvalid && k >= m && k < n) {
+        float* s = slot + (k - m) * 2048 + lane;
+#pragma unroll
+        for (int b = 0; b < 32; ++b) s[b * 64] = acc[b];
+      }
+      lds_barrier();
+      if (wvalid && k < n - m) {
+        const float* s = slot + k * 2048 + lane;
+#pragma unroll
+        for (int b = 0; b < 32; ++b) acc[b] += s[b * 64];
+      }
+      lds_barrier();
+      n = m;
+    }
+    if (wvalid && k == 0) {
+#pragma unroll
+      for (int b = 0; b < 32; ++b) cs[h * 32 * kGfColPitch + b * kGfColPitch + lane] = acc[b];
+    }
+    lds_barrier();
+    // ---- Adam on the own columns (w before the step counts in the loss's |w| sum)
+    double aw = 0.0;
+    for (int e = tid; e < CH * 2048; e += kGfThreads) {
+      const int hh = e >> 11, el = e & 2047;
+      if (hh < nch && c_lo + e < a.cols) {
+        const float gsum = cs[hh * 32 * kGfColPitch + (el & 31) * kGfColPitch + (el >> 5)];
+        float w = Wv[e], m = Mv[e], v = Vv[e];
+        aw += fabs(static_cast<double>(w));
+        const float sgn = w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f);
+        float gr = fmaf(l1s, sgn, gsum);
+        gr = fmaf(a.P.weight_decay, w, gr);
+        m = fmaf(1.f - a.P.beta1, gr - m, m);
+        v = fmaf(1.f - a.P.beta2, gr * gr, v * a.P.beta2);
+        const float denom = sqrtf(v) / sc.bc2_sqrt + a.P.eps;
+        w = w - sc.step_size * (m / denom);
+        Wv[e] = w;
+        Mv[e] = m;
+        Vv[e] = v;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) aw += __shfl_xor(aw, o);
+    if (lane == 0) red[wave] = aw;
+    lds_barrier();
+    if (tid == 0) {
+      double s = 0.0;
+      for (int i = 0; i < kGfWaves; ++i) s += red[i];
+      a.aw_part[(int64_t)t * a.nwg + wg] = s;
+    }
+    build_w_tables();
+    lds_barrier();
+  }
+  if (aborted) return;
+  for (int e = tid; e < CH * 2048; e += kGfThreads) {
+    const int64_t c = c_lo + e;
+    if ((e >> 11) < nch && c < a.cols) {
+      a.wg[c] = Wv[e];
+      a.mg[c] = Mv[e];
+      a.vg[c] = Vv[e];
+    }
+  }
+}
 
 // Also hands the fit's status word to the caller: the multi-workgroup exchange's error word, or 0.
 __global__ void k_argmin_first(const double* __restrict__ v, int64_t n, int32_t* __restrict__ out,
@@ -6292,13 +6647,17 @@ struct WlmWs {
   bool grid;
   int n_wg, n_tk;
   size_t ppart_off, g_off, tk_off, aw_off, lds_p, lds_g;
+  // fused grid fit (k_gw_fused): chunks per workgroup, padded row blocks, workgroups, LDS bytes
+  bool gf;
+  int gf_ch, gf_nrbp, gf_nwg;
+  size_t gf_lds, gfx_off, gferr_off;
 };
 
 static bool wlm_env(const char* v) {
   const char* env = getenv("XPG_WLM");
   return env && std::strcmp(env, v) == 0;
 }
-static bool wlm_force_grid() { return wlm_env("grid"); }
+static bool wlm_force_grid() { return wlm_env("grid") || wlm_env("grid3"); }
 
 
 // Word slices per wave item: minimise (rounds of 16 waves) x (words per item + 1 for the item's
@@ -6316,6 +6675,31 @@ static int wlm_slices(int64_t blocks, int words) {
   return best;
 }
 
+// The fused grid fit takes a shape when a workgroup's waves can hold every 32-row block of its
+// chunks in registers (two blocks per wave, 16 waves) and the chunks fit on the device's CUs one
+// workgroup each; XPG_WLM=grid3 keeps the three-launch steps (A/B, tests).
+static void wlm_plan_fused(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
+  L->gf = false;
+  if (wlm_env("grid3")) return;
+  const int64_t words = cdiv(cols, 32), n_chunks = cdiv(words, kGwWords);
+  const int64_t nrb = cdiv(batch, 32);
+  if (nrb > 32) return;
+  const int nrbp = static_cast<int>(cdiv(nrb, kGfTpw) * kGfTpw), nwc = nrbp / kGfTpw;
+  const int ch_max = std::min(kGfMaxCh, kGfWaves / nwc);
+  if (ch_max < 1 || rows > INT32_MAX || cols > INT32_MAX) return;
+  const int64_t cus = device_cus();
+  const int64_t ch = cdiv(n_chunks, cus);
+  if (ch > ch_max) return;
+  const GfLds G = gf_lds(static_cast<int>(ch), nrbp);
+  const size_t lds = sizeof(float) * (size_t)G.total + 2 * kGfWaves * sizeof(double);
+  if (lds > 160 * 1024) return;
+  L->gf = true;
+  L->gf_ch = static_cast<int>(ch);
+  L->gf_nrbp = nrbp;
+  L->gf_nwg = static_cast<int>(cdiv(n_chunks, ch));
+  L->gf_lds = std::max<size_t>(lds, 81 * 1024);  // > half the CU's LDS: one workgroup per CU
+}
+
 static int wlm_layout_grid(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, WlmWs* L) {
   const int64_t steps = cdiv(rows, batch);
   const int64_t words = cdiv(cols, 32);
@@ -6326,6 +6710,9 @@ static int wlm_layout_grid(int64_t n_fits, int64_t rows, int64_t cols, int64_t b
   L->n_tk = static_cast<int>(cdiv(batch, 64));
   L->lds_p = 0;  // static
   L->lds_g = sizeof(float) * (size_t)(((16 * ((((batch + 31) / 32) * 8) | 1) + 3) & ~3) + 32 * 65);
+  wlm_plan_fused(rows, cols, batch, L);
+  const int n_part = L->gf ? std::max(L->n_wg, L->gf_nwg) : L->n_wg;  // aw partials per step
+  const int n_tkp = L->gf ? std::max(L->n_tk, L->gf_nwg) : L->n_tk;  // loss-term partials per step
   const size_t F = static_cast<size_t>(n_fits);
   size_t off = 0;
   L->steps_off = off;
@@ -6337,9 +6724,13 @@ static int wlm_layout_grid(int64_t n_fits, int64_t rows, int64_t cols, int64_t b
   L->phist_off = off;
   off += align_up(F * sizeof(float) * (size_t)rows);
   L->tk_off = off;
-  off += align_up(F * sizeof(double) * (size_t)steps * L->n_tk);
+  off += align_up(F * sizeof(double) * (size_t)steps * n_tkp);
   L->aw_off = off;
-  off += align_up(F * sizeof(double) * (size_t)steps * L->n_wg);
+  off += align_up(F * sizeof(double) * (size_t)steps * n_part);
+  L->gfx_off = off;  // fused: per fit [batch][nwg] p granules + [batch] g granules
+  off += align_up(L->gf ? F * sizeof(uint64_t) * (size_t)batch * (L->gf_nwg + 1) : 0);
+  L->gferr_off = off;
+  off += align_up(L->gf ? sizeof(uint32_t) : 0);
   L->total = off;
   return XPG_OK;
 }
@@ -6456,6 +6847,54 @@ static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   float* p_hist = reinterpret_cast<float*>(ws + L.phist_off);
   double* tk_part = reinterpret_cast<double*>(ws + L.tk_off);
   double* aw_part = reinterpret_cast<double*>(ws + L.aw_off);
+  if (L.gf) {
+    uint64_t* gx = reinterpret_cast<uint64_t*>(ws + L.gfx_off);
+    uint32_t* err = reinterpret_cast<uint32_t*>(ws + L.gferr_off);
+    const int64_t n_gx = (int64_t)batch * (L.gf_nwg + 1);
+    // per-step constants + granule / error-word clearing, one launch
+    hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib,
+                       P, step0, stp, gx, n_gx * n_fits, err, 1);
+    XPG_LAUNCHED();
+    // test hooks (diagnostics switches, as the multi-workgroup fit): XPG_MC_SPIN (poll bound),
+    // XPG_MC_FAULT = k >= 1 (workgroup k - 1 of fit 0 skips its first publish)
+    int spin_env = 0, fault_env = 0;
+    if (const int rc = diag_env("XPG_MC_SPIN", &spin_env)) return rc;
+    if (const int rc = diag_env("XPG_MC_FAULT", &fault_env)) return rc;
+    XPG_HIP(lds_limit(reinterpret_cast<const void*>(&k_gw_fused)));
+    for (int64_t f = 0; f < n_fits; ++f) {  // one persistent launch per fit, in stream order
+      GfArgs a;
+      a.bits = bits + f * rows * words;
+      a.rows = static_cast<int>(rows);
+      a.cols = static_cast<int>(cols);
+      a.words = static_cast<int>(words);
+      a.steps = static_cast<int>(steps);
+      a.batch = ib;
+      a.ch = L.gf_ch;
+      a.nrbp = L.gf_nrbp;
+      a.nwg = L.gf_nwg;
+      a.fault_wg = (f == 0 && fault_env > 0) ? fault_env - 1 : -1;
+      a.spin_limit = spin_env > 0 ? static_cast<uint32_t>(spin_env) : kMcSpinLimit;
+      a.kern = kernel + f * rows;
+      a.stp = stp + f * steps;
+      a.P = P;
+      a.wg = w + f * cols;
+      a.mg = adam_m + f * cols;
+      a.vg = adam_v + f * cols;
+      a.p_hist = p_hist + f * rows;
+      a.tk_part = tk_part + f * steps * L.gf_nwg;
+      a.aw_part = aw_part + f * steps * L.gf_nwg;
+      a.xp = gx + f * n_gx;
+      a.err = err;
+      hipLaunchKernelGGL(k_gw_fused, dim3(static_cast<unsigned>(L.gf_nwg)), dim3(kGfThreads), L.gf_lds, st, a);
+      XPG_LAUNCHED();
+    }
+    hipLaunchKernelGGL(k_gw_loss, dim3(static_cast<unsigned>(steps), nf), dim3(64), 0, st, tk_part, L.gf_nwg,
+                       aw_part, L.gf_nwg, stp, rows, cols, ib, P.l1_lambda, losses);
+    XPG_LAUNCHED();
+    hipLaunchKernelGGL(k_argmin_first, dim3(nf), dim3(64), 0, st, losses, steps, best_epoch, err, status);
+    XPG_LAUNCHED();
+    return XPG_OK;
+  }
   hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib, P,
                      step0, stp, nullptr, int64_t(0), nullptr, 0);
   XPG_LAUNCHED();
@@ -6492,8 +6931,8 @@ int xpg_wlm_plan(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, int3
   WlmWs L;
   int rc = wlm_layout(n_fits, rows, cols, batch, &L);
   if (rc) return rc;
-  *kind = L.grid ? XPG_WLM_GRID : (L.mc ? XPG_WLM_MULTI : XPG_WLM_SINGLE);
-  *parts = L.mc && !L.grid ? L.P : 1;
+  *kind = L.grid ? (L.gf ? XPG_WLM_GRID_FUSED : XPG_WLM_GRID) : (L.mc ? XPG_WLM_MULTI : XPG_WLM_SINGLE);
+  *parts = L.grid ? (L.gf ? L.gf_nwg : 1) : (L.mc ? L.P : 1);
   return XPG_OK;
 }
 

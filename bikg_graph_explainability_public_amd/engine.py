@@ -987,13 +987,15 @@ def check_status_host(h):
         check_fit_status(torch.ones(1, dtype=torch.int32))
 
 
-WLM_KINDS = {0: "single", 1: "multi", 2: "grid"}
+WLM_KINDS = {0: "single", 1: "multi", 2: "grid", 3: "grid_fused"}
 
 
 def wlm_plan(n_fits, rows, cols, batch):
     """(kind, parts) of the fit kernel a shape takes on the current device (xpg_wlm_plan):
-    kind "single" (one workgroup per fit), "multi" (`parts` co-resident workgroups per fit) or
-    "grid" (the many-column streaming fit, which has no prepared form)."""
+    kind "single" (one workgroup per fit), "multi" (`parts` co-resident workgroups per fit),
+    "grid" (the many-column streaming fit, three launches per step) or "grid_fused" (the
+    many-column fit as one persistent launch per fit over `parts` workgroups); the grid kinds
+    have no prepared form."""
     kind, parts = ctypes.c_int32(0), ctypes.c_int32(0)
     _lib.check(_lib.load().xpg_wlm_plan(int(n_fits), int(rows), int(cols), int(batch),
                                         ctypes.byref(kind), ctypes.byref(parts)))
@@ -1012,7 +1014,7 @@ class PreparedFit:
 
     def __init__(self, n_fits, rows, cols, batch, params, device):
         self.kind, self.parts = wlm_plan(n_fits, rows, cols, batch)
-        if self.kind == "grid":
+        if self.kind.startswith("grid"):
             raise ValueError(f"PreparedFit: {cols} columns take the many-column grid fit, which "
                              "has no prologue / prepared form; use wlm_fit")
         self.shape = (int(n_fits), int(rows), int(cols), int(batch))

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define XPG_ABI_VERSION 20
+#define XPG_ABI_VERSION 21
 #define XPG_MAX_TERMS 8
 
 typedef void* xpg_stream_t; /* hipStream_t */
@@ -288,10 +288,13 @@ typedef struct xpg_wlm_params {
 /* Workspace needed by xpg_wlm_fit. */
 int xpg_wlm_workspace(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, size_t* bytes);
 /* Which fit kernel a shape takes (v13): *kind = XPG_WLM_SINGLE (one workgroup per fit),
- * XPG_WLM_MULTI (*parts co-resident workgroups per fit) or XPG_WLM_GRID (the many-column
- * streaming fit: no xpg_wlm_prepare / xpg_wlm_fit_prepared); *parts = 1 unless MULTI.  The
- * choice depends on the current device's CU count and the XPG_WLM / XPG_MC_* overrides. */
-enum xpg_wlm_kind { XPG_WLM_SINGLE = 0, XPG_WLM_MULTI = 1, XPG_WLM_GRID = 2 };
+ * XPG_WLM_MULTI (*parts co-resident workgroups per fit), XPG_WLM_GRID (the many-column
+ * streaming fit, three launches per Adam step) or XPG_WLM_GRID_FUSED (v21: the many-column fit
+ * as one persistent launch per fit, *parts co-resident workgroups, one per CU; the grid kinds
+ * have no xpg_wlm_prepare / xpg_wlm_fit_prepared); *parts = 1 unless MULTI / GRID_FUSED.  The
+ * choice depends on the current device's CU count and the XPG_WLM / XPG_MC_* overrides
+ * (XPG_WLM=grid3: the three-launch grid fit). */
+enum xpg_wlm_kind { XPG_WLM_SINGLE = 0, XPG_WLM_MULTI = 1, XPG_WLM_GRID = 2, XPG_WLM_GRID_FUSED = 3 };
 int xpg_wlm_plan(int64_t n_fits, int64_t rows, int64_t cols, int64_t batch, int32_t* kind,
                  int32_t* parts);
 /* Runs ceil(rows / batch) Adam steps of train_model over consecutive row batches for n_fits

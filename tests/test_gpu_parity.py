@@ -649,13 +649,16 @@ def test_wlm_fit_vs_reference(name, wlm_path, monkeypatch):
                                    (3000, 1193, 256),   # short last batch (quirk Q7)
                                    (2000, 700, 100),    # batch not a multiple of 32
                                    (640, 4100, 64)])    # > 4096 columns
-@pytest.mark.parametrize("wlm_path", ["single", "mc", "grid"])
+@pytest.mark.parametrize("wlm_path", ["single", "mc", "grid", "grid3"])
 def test_wlm_fit_vs_oracle_large(R, S, B, wlm_path, monkeypatch):
     """Fresh data vs the fp64 oracle at sizes the golden fixtures do not reach, through each of
-    the three fit kernels: one workgroup per fit (XPG_WLM=single), P co-resident workgroups per
-    fit (mc, the default from 256 columns) and the many-column grid fit (S > 16384)."""
+    the fit kernels: one workgroup per fit (XPG_WLM=single), P co-resident workgroups per fit
+    (mc, the default from 256 columns), the many-column grid fit (S > 16384) as one persistent
+    launch (grid: k_gw_fused) and as three launches per step (grid3)."""
     monkeypatch.setenv("XPG_WLM", wlm_path)
     e = _eng()
+    if wlm_path.startswith("grid"):
+        assert e.wlm_plan(1, R, S, B)[0] == ("grid_fused" if wlm_path == "grid" else "grid")
     rng = np.random.default_rng(11)
     m = rng.random((R, S)) < 0.5
     y = rng.random(R).astype(np.float32)
@@ -714,6 +717,82 @@ def test_wlm_fit_many_columns_vs_oracle():
         assert int(best[f]) == rb
 
 
+@pytest.mark.parametrize("F,R,S,B", [(1, 2500, 20_000, 1000),   # 32 row blocks: one chunk per workgroup
+                                     (1, 1100, 70_000, 96),     # 3 row blocks, short last batch
+                                     (3, 1024, 17_000, 512)])   # 3 fits: one launch each
+def test_wlm_fit_fused_grid_shapes_vs_oracle(F, R, S, B):
+    """The persistent many-column fit (k_gw_fused) on shapes at its limits vs the fp64 oracle:
+    the largest batch it holds in registers, a batch that is not a multiple of 32 with a short
+    last batch, several fits in one call."""
+    e = _eng()
+    kind, parts = e.wlm_plan(F, R, S, B)
+    assert kind == "grid_fused" and parts >= 1, (kind, parts)
+    rng = np.random.default_rng(21)
+    m = rng.random((F, R, S)) < 0.5
+    y = rng.random((F, R)).astype(np.float32)
+    k = np.stack([oracle.shap_kernel(m[f]) for f in range(F)])
+    w0 = ((rng.random((F, S)) - 0.5) * 0.02).astype(np.float32)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    bits = torch.stack([e.pack_masks(torch.as_tensor(m[f]).to(DEV)) for f in range(F)])
+    w, losses, best, _, _ = e.wlm_fit(bits, S, B, torch.as_tensor(y), torch.as_tensor(k),
+                                      torch.as_tensor(w0), params)
+    for f in range(F):
+        ref, rl, rb = oracle.train_wlm(m[f], B, y[f], k[f], w0[f], params)
+        np.testing.assert_allclose(w[f].cpu().numpy(), ref, rtol=0, atol=1e-4)
+        np.testing.assert_allclose(losses[f].cpu().numpy(), rl, rtol=1e-5)
+        assert int(best[f]) == rb
+
+
+@pytest.mark.parametrize("R", [2560, 2300])
+def test_wlm_fit_fused_grid_c3_scale_vs_three_launch(R, monkeypatch):
+    """graph_prediction at the c3 size (S = 1M columns, batch 512: 512 chunks on 256 workgroups,
+    every workgroup a reducer): the persistent fit vs the three-launch grid fit, which the oracle
+    pins at smaller S; R = 2300 ends with a short batch.  Same weights within 1e-5 (the two sum
+    the same products in different orders), same losses within 1e-6 relative, same best epoch."""
+    e = _eng()
+    S, B = 1_000_000, 512
+    g = torch.Generator(device=DEV).manual_seed(5)
+    bits = e.pack_masks(torch.rand((R, S), generator=g, device=DEV) < 0.5)
+    y = torch.rand(R, generator=g, device=DEV)
+    k = torch.rand(R, generator=g, device=DEV, dtype=torch.float64) + 0.5
+    w0 = (torch.rand(S, generator=g, device=DEV) - 0.5) * 0.02
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    assert e.wlm_plan(1, R, S, B)[0] == "grid_fused"
+    w1, l1, b1, m1, v1 = e.wlm_fit(bits, S, B, y, k, w0, params)
+    monkeypatch.setenv("XPG_WLM", "grid3")
+    w3, l3, b3, m3, v3 = e.wlm_fit(bits, S, B, y, k, w0, params)
+    assert float((w1 - w3).abs().max()) <= 1e-5
+    np.testing.assert_allclose(l1.cpu().numpy(), l3.cpu().numpy(), rtol=1e-6)
+    assert int(b1[0]) == int(b3[0])
+    assert float((m1 - m3).abs().max()) <= 1e-5
+
+
+def test_wlm_fit_fused_grid_exchange_failure_raises(monkeypatch):
+    """A workgroup of the persistent many-column fit that never publishes (test hook) ends the
+    fit with the error word set: FitExchangeError, and a clean fit afterwards matches the oracle."""
+    from bikg_graph_explainability_public_amd import _lib
+    e = _eng()
+    rng = np.random.default_rng(4)
+    R, S, B = 600, 20_000, 128
+    m = rng.random((R, S)) < 0.5
+    y = rng.random(R).astype(np.float32)
+    k = oracle.shap_kernel(m)
+    w0 = ((rng.random(S) - 0.5) * 0.05).astype(np.float32)
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    bits = e.pack_masks(torch.as_tensor(m).to(DEV))
+    args = (bits, S, B, torch.as_tensor(y), torch.as_tensor(k), torch.as_tensor(w0), params)
+    assert e.wlm_plan(1, R, S, B)[0] == "grid_fused"
+    monkeypatch.setenv("XPG_DIAGNOSTICS", "1")
+    monkeypatch.setenv("XPG_MC_SPIN", "20000")
+    monkeypatch.setenv("XPG_MC_FAULT", "3")
+    with pytest.raises(_lib.FitExchangeError):
+        e.wlm_fit(*args)
+    monkeypatch.delenv("XPG_MC_FAULT")
+    w, _, _, _, _ = e.wlm_fit(*args)
+    ref, _, _ = oracle.train_wlm(m, B, y, k, w0, params)
+    np.testing.assert_allclose(w.cpu().numpy(), ref, rtol=0, atol=1e-4)
+
+
 @pytest.mark.parametrize("F,S", [(5, 200), (11, 700)])
 @pytest.mark.parametrize("wlm_path", ["single", "mc"])
 def test_wlm_fit_batched_independent_fits(wlm_path, F, S, monkeypatch):
@@ -738,7 +817,7 @@ def test_wlm_fit_batched_independent_fits(wlm_path, F, S, monkeypatch):
         assert int(best[f]) == rb
 
 
-@pytest.mark.parametrize("wlm_path", ["single", "mc", "grid"])
+@pytest.mark.parametrize("wlm_path", ["single", "mc", "grid", "grid3"])
 def test_wlm_fit_continuation_equals_one_fit(wlm_path, monkeypatch):
     """A fresh fit (xpg_wlm_fit_from: w = w0, zero moments written by the fit's prologue) over
     rows [0, R) gives bitwise the weights of the fit split in two calls: xpg_wlm_fit_from over
