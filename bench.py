@@ -1219,13 +1219,16 @@ def c5_section(args, dev, world, rank):
 
 # ----------------------------------------------------------------------------- N = 1 sections
 GP_KERNELS = ("k_wlm_stats", "k_gw_p", "k_gw_g", "k_gw_grad", "k_gw_loss", "k_argmin_first")
+GP_FUSED_KERNELS = ("k_wlm_stats", "k_gw_fused", "k_gw_loss", "k_argmin_first")
 
 
 def graph_prediction_section(args, dev):
     """The reference's graph_prediction semantics on the c3 graph (explainer.py:427-447: no
     subgraph, S = N = 1M mask columns) for one query node, one repeat of interpret_samples=512,
     epochs=50 (25,600 rows): device sampler with fused row counts -> receptive-field forward ->
-    KernelSHAP -> many-column surrogate fit (k_gw_*: streams the step's mask bits twice)."""
+    KernelSHAP -> many-column surrogate fit (k_gw_fused: one persistent launch, each step's mask
+    bits read once; XPG_WLM=grid3: the three-launch k_gw_p / k_gw_g / k_gw_grad steps, which
+    stream them twice)."""
     from bikg_graph_explainability_public_amd import engine, pipeline
     x, ei, arch = c3_graph(dev)
     N = x.shape[0]
@@ -1259,14 +1262,20 @@ def graph_prediction_section(args, dev):
           for j, name in enumerate(("sample", "forward", "shap", "wlm"))}
     total = sum(ph.values())
     W = (N + 31) // 32
-    wbytes = 2 * R * W * 4 + epochs * 6 * N * 4  # mask bits twice per step + Adam state r/w
+    kind, parts = engine.wlm_plan(1, R, N, batch)
+    if kind == "grid_fused":  # bits once per step; w / m / v read and written once per fit
+        wbytes, kernels = R * W * 4 + 6 * N * 4, GP_FUSED_KERNELS
+        formula = "R x ceil(S/32) x 4 (bits, read once) + 24 S (w, m, v read + write, once per fit)"
+    else:
+        wbytes, kernels = 2 * R * W * 4 + epochs * 6 * N * 4, GP_KERNELS
+        formula = "2 x R x ceil(S/32) x 4 (bits, p and grad passes) + steps x 24 S (w, m, v read + write)"
     return {"workload": "c3 graph_prediction, one query (node 7), S = 1M mask columns, "
                         "interpret_samples=512 x epochs=50 = 25,600 rows, one repeat",
             "ms_per_repeat": total, "samples_per_s": R / (total * 1e-3), "phases_ms": ph,
-            "roofline": dict(roofline(wbytes, ph["wlm"] * 1e-3, "gp", GP_KERNELS),
-                             kernel="many-column surrogate fit (" + ", ".join(GP_KERNELS) + ")",
-                             bytes_formula="2 x R x ceil(S/32) x 4 (bits, p and grad passes) + "
-                                           "steps x 24 S (w, m, v read + write)"),
+            "surrogate_fit": "%s (%d workgroup(s) per fit)" % (kind, parts),
+            "roofline": dict(roofline(wbytes, ph["wlm"] * 1e-3, "gp", kernels),
+                             kernel="many-column surrogate fit (" + ", ".join(kernels) + ")",
+                             bytes_formula=formula),
             "sampler_GBps": R * W * 4 / (ph["sample"] * 1e-3) / 1e9}
 
 

@@ -4722,28 +4722,33 @@ __device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lan
 }
 
 // Sum of v[0..7] over the wave's 64 lanes for every i: after the call lanes 8i..8i+7 hold
-// sum_lanes v[i] (3 halving exchange stages, then 3 butterfly stages over the 8-lane groups).
-__device__ __forceinline__ float wave_transpose_reduce8(float (&v)[8], int lane) {
+// sum_lanes v[i] (k_gw_fused).  wave_transpose_reduce32's halving stages without LDS permutes:
+// the 32- and 16-lane stages are v_permlane32_swap / v_permlane16_swap (swapping the two halves'
+// values IS the stage's keep / send exchange), the 8-lane stage a DPP row rotation, then a DPP
+// half-mirror and two quad permutes sum the 8 lanes that share a row.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_transpose_reduce8_pl(float (&v)[8], int lane) {
 #pragma unroll
-  for (int st = 0; st < 3; ++st) {
-    const int half = 4 >> st;
-    const int xm = 32 >> st;
-    const bool hi = (lane & xm) != 0;
-#pragma unroll
-    for (int k = 0; k < half; ++k) {
-      float lo_v = v[k], hi_v = v[k + half];
-      asm volatile("" : "+v"(lo_v), "+v"(hi_v));
-      const float keep = hi ? hi_v : lo_v;
-      const float send = hi ? lo_v : hi_v;
-      float r = keep + __shfl_xor(send, xm);
-      asm volatile("" : "+v"(r));
-      v[k] = r;
-    }
+  for (int k = 0; k < 4; ++k) {  // lanes 0-31 keep v[k], lanes 32-63 v[k + 4]
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 4]), false, false);
+    v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
-  float r = v[0];
-  r += __shfl_xor(r, 4);
-  r += __shfl_xor(r, 2);
-  r += __shfl_xor(r, 1);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // even 16-lane rows keep v[k], odd rows v[k + 2]
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 2]), false, false);
+    v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const bool hi = (lane & 8) != 0;  // lanes l and l ^ 8 of a row: row_ror:8
+  float lo_v = v[0], hi_v = v[1];
+  asm volatile("" : "+v"(lo_v), "+v"(hi_v));
+  const float keep = hi ? hi_v : lo_v, send = hi ? lo_v : hi_v;
+  float r = keep + dpp_mov<0x128>(send);
+  r += dpp_mov<0x141>(r);  // row_half_mirror: l <-> 7 - l
+  r += dpp_mov<0x4E>(r);   // quad_perm [2,3,0,1]
+  r += dpp_mov<0xB1>(r);   // quad_perm [1,0,3,2]
   return r;
 }
 
@@ -4997,7 +5002,11 @@ constexpr int kGfMaxCh = 2;        // chunks per workgroup (LDS: w tables + w / 
 constexpr int kGfWaves = 8;        // waves per workgroup
 constexpr int kGfTpw = 4;          // resident 32-row blocks per wave
 constexpr int kGfThreads = kGfWaves * 64;
+constexpr int kGfLook1 = 8;        // phase 1: rows whose 8 lookups issue together
+constexpr int kGfLook3 = 4;        // phase 3: columns whose 8 lookups issue together (acc[32] live)
 constexpr int kGfColPitch = 65;    // column-sum image [b][j] pitch: conflict-free both ways
+constexpr int kGfSlot = 32 * kGfColPitch;  // one wave's column-sum slot (floats)
+constexpr int kGfMaxWg = 512;      // workgroups per fit (a reducer lane polls nwg / 64 granules)
 
 struct GfArgs {
   const uint32_t* bits;
@@ -5010,29 +5019,44 @@ struct GfArgs {
   xpg_wlm_params P;
   int rows, cols, words, steps, batch, ch, nrbp, nwg, fault_wg;
   uint32_t spin_limit;
+#ifdef XPG_GF_STAMPS
+  int dbg;  // diagnostics build: 1 = no next-step bit loads (compute alone)
+#endif
 };
 
 // LDS image of k_gw_fused (floats): [R0: w tables | tree slots][cs][w][m][v][pp][gb][G] + doubles.
 // nrbp = row blocks rounded up to kGfTpw; a chunk has nrbp / kGfTpw waves.
 struct GfLds {
-  int r0, cs, w, m, v, pp, gb, G, gp, slots, total;  // float offsets; total in floats (doubles follow)
+  int r0, w, m, v, pp, gb, G, total;  // float offsets; total in floats (doubles follow)
 };
 __host__ __device__ inline GfLds gf_lds(int ch, int nrbp) {
   GfLds L;
-  const int nwc = nrbp / kGfTpw, slots = nwc / 2 > 4 ? nwc / 2 : 4;
-  L.gp = (nrbp * 8) | 1;
-  L.slots = slots;
+  const int nwc = nrbp / kGfTpw, r0 = ch * (nwc * kGfSlot > 8 * 16 * 64 ? nwc * kGfSlot : 8 * 16 * 64);
   int o = 0;
-  L.r0 = o;  o += ch * slots * 2048;  // >= ch * 8 * 16 * 64 (the w tables)
-  L.cs = o;  o += ch * 32 * kGfColPitch;
+  L.r0 = o;  o += (r0 + 15) & ~15;  // the w tables | the waves' column-sum slots
   L.w = o;   o += ch * 2048;
   L.m = o;   o += ch * 2048;
   L.v = o;   o += ch * 2048;
   L.pp = o;  o += ch * nrbp * 32;
   L.gb = o;  o += nrbp * 32;
-  L.G = o;   o += 16 * L.gp;
+  L.G = o;   o += 16 * nrbp * 8;
   L.total = (o + 1) & ~1;
   return L;
+}
+
+// x >> sh for sh >= 0, x << -sh otherwise (sh a compile-time constant after unrolling)
+__device__ __forceinline__ uint32_t shr_i(uint32_t x, int sh) { return sh >= 0 ? x >> sh : x << -sh; }
+// (x & m) | b in one v_and_or_b32 (the compiler turns a disjoint or into an add and then adds
+// the base separately)
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t b) {
+  uint32_t r;
+  asm volatile("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(m), "v"(b));
+  return r;
+}
+// LDS float at byte address a + imm (imm folded into the instruction's offset)
+__device__ __forceinline__ float lds_f32(uint32_t a, int imm) {
+  typedef __attribute__((address_space(3))) const float lf32;
+  return *reinterpret_cast<lf32*>(static_cast<uintptr_t>(a + imm));
 }
 
 __device__ __forceinline__ float gf_poll(const uint64_t* p, uint32_t tag, uint32_t spin_limit, uint32_t* err,
@@ -5052,14 +5076,33 @@ __device__ __forceinline__ float gf_poll(const uint64_t* p, uint32_t tag, uint32
   return __uint_as_float(static_cast<uint32_t>(v));
 }
 
+#ifdef XPG_GF_STAMPS  // diagnostics build (tools/gf_probe): per-phase s_memtime cycles of thread 0
+__device__ uint64_t g_gf_stamps[1024 * 8];
+#define GF_STAMP(k)                                  \
+  if (tid == 0) {                                    \
+    __builtin_amdgcn_sched_barrier(0);               \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime(); \
+    gst[k] += now_ - glast;                          \
+    glast = now_;                                    \
+    __builtin_amdgcn_sched_barrier(0);               \
+  }
+#else
+#define GF_STAMP(k)
+#endif
+
 __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
   extern __shared__ __attribute__((aligned(16))) float gsm[];
+#ifdef XPG_GF_STAMPS
+  uint64_t gst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, glast = __builtin_amdgcn_s_memtime();
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform roles and row blocks
   const int wg = blockIdx.x, CH = a.ch, nwc = a.nrbp / kGfTpw;
   const GfLds L = gf_lds(CH, a.nrbp);
   double* red = reinterpret_cast<double*>(gsm + L.total);  // [kGfWaves] aw, [kGfWaves] tk
-  __shared__ int abort_s;
+  // abort flag after the doubles: no static LDS, so the image (and the w tables) start at LDS
+  // address 0 and a table address is an and-or of the shifted nibble with the lane's base
+  int& abort_s = *reinterpret_cast<int*>(red + 2 * kGfWaves);
   if (tid == 0) abort_s = 0;
   const int n_chunks = (a.words + kGwWords - 1) / kGwWords;
   const int chunk0 = wg * CH;
@@ -5073,14 +5116,12 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
   const uint32_t wd = static_cast<uint32_t>(w0 + (lane < nw ? lane : 0));
   const int64_t c_lo = (int64_t)chunk0 * 2048;  // first own column
   float* Wt = gsm + L.r0;
-  float* cs = gsm + L.cs;
   float* Wv = gsm + L.w;
   float* Mv = gsm + L.m;
   float* Vv = gsm + L.v;
   float* pp = gsm + L.pp;
   float* gb = gsm + L.gb;
   float* G = gsm + L.G;
-  const int gp = L.gp;
   const int RB = a.nrbp * 32;
   const uint32_t pitch = static_cast<uint32_t>(a.words) * 4u;
 
@@ -5130,138 +5171,190 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
 
   const float l1s = a.P.l1_lambda / static_cast<float>(a.cols);
   bool aborted = false;
+  // Rows split in two halves by row block (rb & 3 < 2: the waves' blocks u = 0, 1; else u = 2, 3)
+  // so the exchanges overlap compute: half 0's partials travel while half 1's phase 1 runs, half
+  // 1's g values while half 0's phase 3 runs
+  auto half_of_row = [](int r) { return ((r >> 5) & 3) >> 1; };
   for (int t = 0; t < a.steps; ++t) {
     const WlmStep sc = a.stp[t];
     const int64_t r0 = (int64_t)t * a.batch;
     const int B = static_cast<int>(min((int64_t)a.batch, (int64_t)a.rows - r0));
     const uint32_t tag = static_cast<uint32_t>(t + 1);
-    // ---- phase 1: chunk partials of p over the own words, 8 rows at a time
-    if (wvalid) {
-      const float* Tl = Wt + h * 8 * 16 * 64 + lane;
+    GF_STAMP(7)
+    double tk = 0.0;
 #pragma unroll
-      for (int u = 0; u < kGfTpw; ++u) {
-        const int rb = kGfTpw * k + u;
-        const int nr = min(32, B - rb * 32);
-        if (nr > 0) {
+    for (int H = 0; H < 2; ++H) {
+      // ---- phase 1 (this half's blocks): chunk partials of p over the own words, 8 rows at a time
+      if (wvalid) {
+        // table entry (q, v) of this lane's word: byte (h * 8 + q) * 4096 + v * 256 + lane * 4 of
+        // the table image (at LDS offset 0), so the nibble lands in bits 8-11 with one shift and
+        // one and-or
+        const uint32_t tb = static_cast<uint32_t>(h * 8 * 16 * 64 + lane) * 4u;
 #pragma unroll
-          for (int i0 = 0; i0 < 32; i0 += 8) {
-            float c[8];
+        for (int u = 2 * H; u < 2 * H + 2; ++u) {
+          const int rb = kGfTpw * k + u;
+          const int nr = min(32, B - rb * 32);
+          if (nr > 0) {
+            // rows past the batch and words past the chunk read as 0 (here and in phase 3)
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const uint32_t xi = i0 + i < nr ? (x[u][i0 + i] & lmask) : 0u;
-              float s = 0.f;
+            for (int i = 0; i < 32; ++i) x[u][i] = i < nr ? (x[u][i] & lmask) : 0u;
 #pragma unroll
-              for (int q = 0; q < 8; ++q) s += Tl[(q * 16 + ((xi >> (4 * q)) & 15u)) * 64];
-              c[i] = s;
+            for (int i0 = 0; i0 < 32; i0 += 8) {
+              // the lookups of kGfLook1 rows issued before their adds (a chained add per lookup
+              // kept one LDS read in flight)
+              float c[8];
+#pragma unroll
+              for (int i1 = 0; i1 < 8; i1 += kGfLook1) {
+                float v[kGfLook1][8];
+#pragma unroll
+                for (int i = 0; i < kGfLook1; ++i)
+#pragma unroll
+                  for (int q = 0; q < 8; ++q)
+                    v[i][q] = lds_f32(and_or(shr_i(x[u][i0 + i1 + i], 4 * q - 8), 0xf00u, tb), q * 4096);
+#pragma unroll
+                for (int i = 0; i < kGfLook1; i += 2) {  // two rows per packed add
+                  f32x2 s2 = {v[i][0], v[i + 1][0]};
+#pragma unroll
+                  for (int q = 1; q < 8; ++q) s2 += f32x2{v[i][q], v[i + 1][q]};
+                  c[i1 + i] = s2.x;
+                  c[i1 + i + 1] = s2.y;
+                }
+              }
+              const float tot = wave_transpose_reduce8_pl(c, lane);  // row i0 + (lane >> 3)
+              const int i = i0 + (lane >> 3);
+              if (!(lane & 7) && i < nr) pp[h * RB + rb * 32 + i] = tot;
             }
-            const float tot = wave_transpose_reduce8(c, lane);  // row i0 + (lane >> 3)
-            const int i = i0 + (lane >> 3);
-            if (!(lane & 7) && i < nr) pp[h * RB + rb * 32 + i] = tot;
           }
         }
       }
-    }
-    lds_barrier();
-    // ---- publish the workgroup's partial of every row (chunks added in order)
-    if (!(a.fault_wg == wg && t == 0)) {
-      for (int r = tid; r < B; r += kGfThreads) {
-        float v = 0.f;
-        for (int hh = 0; hh < nch; ++hh) v += pp[hh * RB + r];
-        st64_sc1(a.xp + (int64_t)r * a.nwg + wg, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(v));
+      lds_barrier();
+      // ---- publish the workgroup's partial of every row of the half (chunks added in order)
+      if (!(a.fault_wg == wg && t == 0)) {
+        for (int r = tid; r < B; r += kGfThreads) {
+          if (half_of_row(r) != H) continue;
+          float v = 0.f;
+          for (int hh = 0; hh < nch; ++hh) v += pp[hh * RB + r];
+          st64_sc1(a.xp + (int64_t)r * a.nwg + wg, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(v));
+        }
       }
     }
-    // ---- reduce the rows this workgroup owns: p_j, g_j, the loss term
-    double tk = 0.0;
-    for (int j = wg + wave * a.nwg; j < B; j += kGfWaves * a.nwg) {
-      const uint64_t* src = a.xp + (int64_t)j * a.nwg;
-      float part = 0.f;
-      for (int c = lane; c < a.nwg; c += 64) part += gf_poll(src + c, tag, a.spin_limit, a.err, &abort_s);
+    GF_STAMP(0)
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
-      const float p = __shfl(part, 0);
-      if (lane == 0) {
-        const double kj = a.kern[r0 + j];
-        const double d = static_cast<double>(p) - sc.ybar;
-        const float g = static_cast<float>(kj * sc.cg * d);
-        a.p_hist[r0 + j] = p;
-        tk += kj * d * d;
-        st64_sc1(a.xp + (int64_t)a.batch * a.nwg + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(g));
+    for (int H = 0; H < 2; ++H) {
+      // ---- reduce the half's rows this workgroup owns: p_j, g_j, the loss term
+      for (int j = wg + wave * a.nwg; j < B; j += kGfWaves * a.nwg) {
+        if (half_of_row(j) != H) continue;  // wave-uniform
+        const uint64_t* src = a.xp + (int64_t)j * a.nwg;
+        // the lane's granules c = lane + 64 i: all loads in flight first, then any spins
+        uint64_t gr[kGfMaxWg / 64];
+#pragma unroll
+        for (int i = 0; i < kGfMaxWg / 64; ++i)
+          gr[i] = lane + 64 * i < a.nwg ? ld64_sc1(src + lane + 64 * i) : (static_cast<uint64_t>(tag) << 32);
+        float part = 0.f;
+#pragma unroll
+        for (int i = 0; i < kGfMaxWg / 64; ++i)
+          part += static_cast<uint32_t>(gr[i] >> 32) == tag
+                      ? __uint_as_float(static_cast<uint32_t>(gr[i]))
+                      : gf_poll(src + lane + 64 * i, tag, a.spin_limit, a.err, &abort_s);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        const float p = __shfl(part, 0);
+        if (lane == 0) {
+          const double kj = a.kern[r0 + j];
+          const double d = static_cast<double>(p) - sc.ybar;
+          const float g = static_cast<float>(kj * sc.cg * d);
+          a.p_hist[r0 + j] = p;
+          tk += kj * d * d;
+          st64_sc1(a.xp + (int64_t)a.batch * a.nwg + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(g));
+        }
       }
     }
     if (lane == 0) red[kGfWaves + wave] = tk;
-    // ---- the batch's g (rows past B: 0)
-    for (int r = tid; r < RB; r += kGfThreads)
-      gb[r] = r < B ? gf_poll(a.xp + (int64_t)a.batch * a.nwg + r, tag, a.spin_limit, a.err, &abort_s) : 0.f;
-    lds_barrier();
-    if (abort_s) {
-      aborted = true;
-      break;
-    }
-    if (tid == 0) {
-      double s = 0.0;
-      for (int i = 0; i < kGfWaves; ++i) s += red[kGfWaves + i];
-      a.tk_part[(int64_t)t * a.nwg + wg] = s;
-    }
-    for (int e = tid; e < 16 * (a.nrbp * 8); e += kGfThreads) {  // G[v * gp + group]
-      const int v = e / (a.nrbp * 8), grp = e - v * (a.nrbp * 8);
-      const float* gg = gb + 4 * grp;
-      G[v * gp + grp] = ((v & 1) ? gg[0] : 0.f) + ((v & 2) ? gg[1] : 0.f) + ((v & 4) ? gg[2] : 0.f) +
-                        ((v & 8) ? gg[3] : 0.f);
-    }
-    lds_barrier();
-    // ---- phase 3: column sums from the same registers; each block's registers take the next
-    // step's bits as soon as its lookups are done
+    GF_STAMP(1)
+    // ---- phase 3 per half: the half's g (rows past B: 0), its G tables, then column sums from
+    // the same registers; each block's registers take the next step's bits once its lookups are
+    // done
     float acc[32];
 #pragma unroll
     for (int b = 0; b < 32; ++b) acc[b] = 0.f;
 #pragma unroll
-    for (int u = 0; u < kGfTpw; ++u) {
-      const int rb = kGfTpw * k + u;
-      const int nr = min(32, B - rb * 32);
-      if (wvalid && nr > 0) {
+    for (int H = 0; H < 2; ++H) {
+      for (int r = tid; r < RB; r += kGfThreads)
+        if (half_of_row(r) == H)
+          gb[r] = r < B ? gf_poll(a.xp + (int64_t)a.batch * a.nwg + r, tag, a.spin_limit, a.err, &abort_s) : 0.f;
+      lds_barrier();
+      if (H == 0) GF_STAMP(2)
+      if (abort_s) {
+        aborted = true;
+        break;
+      }
+      if (H == 1 && tid == 0) {
+        double s = 0.0;
+        for (int i = 0; i < kGfWaves; ++i) s += red[kGfWaves + i];
+        a.tk_part[(int64_t)t * a.nwg + wg] = s;
+      }
+      for (int e = tid; e < 16 * (a.nrbp * 8); e += kGfThreads) {  // G[group * 16 + v]: a lookup's
+        const int v = e & 15, grp = e >> 4;                          // 16 entries on 16 banks
+        if (half_of_row(grp * 4) != H) continue;
+        const float* gg = gb + 4 * grp;
+        G[e] = ((v & 1) ? gg[0] : 0.f) + ((v & 2) ? gg[1] : 0.f) + ((v & 4) ? gg[2] : 0.f) + ((v & 8) ? gg[3] : 0.f);
+      }
+      lds_barrier();
+      if (H == 0) GF_STAMP(3)
 #pragma unroll
-        for (int i = 0; i < 32; ++i) x[u][i] = i < nr ? (x[u][i] & lmask) : 0u;
-        transpose32(x[u]);  // x[u][b] = column 32 * word + b over the block's rows
-        const float* Gb = G + rb * 8;
+      for (int u = 2 * H; u < 2 * H + 2; ++u) {
+        const int rb = kGfTpw * k + u;
+        const int nr = min(32, B - rb * 32);
+        if (wvalid && nr > 0) {
+          transpose32(x[u]);  // x[u][b] = column 32 * word + b over the block's rows (masked in phase 1)
+          // G[group][v], group = 4 rows: the block's groups at byte gbase + n * 64 (gbase: a
+          // multiple of 64, so the nibble's 4-B slot is an and-or)
+          const uint32_t gbase = static_cast<uint32_t>(L.G + rb * 8 * 16) * 4u;
 #pragma unroll
-        for (int b = 0; b < 32; ++b) {
-          float s = 0.f;
+          for (int b0 = 0; b0 < 32; b0 += kGfLook3) {
+            float v[kGfLook3][8];  // the lookups of kGfLook3 columns in flight, then the adds
 #pragma unroll
-          for (int n = 0; n < 8; ++n) s += Gb[((x[u][b] >> (4 * n)) & 15u) * gp + n];
-          acc[b] += s;
+            for (int b = 0; b < kGfLook3; ++b)
+#pragma unroll
+              for (int n = 0; n < 8; ++n)
+                v[b][n] = lds_f32(and_or(shr_i(x[u][b0 + b], 4 * n - 2), 0x3cu, gbase), n * 64);
+#pragma unroll
+            for (int b = 0; b < kGfLook3; b += 2) {  // two columns per packed add
+              f32x2 s2 = {v[b][0], v[b + 1][0]};
+#pragma unroll
+              for (int n = 1; n < 8; ++n) s2 += f32x2{v[b][n], v[b + 1][n]};
+              f32x2 a2 = {acc[b0 + b], acc[b0 + b + 1]};
+              a2 += s2;
+              acc[b0 + b] = a2.x;
+              acc[b0 + b + 1] = a2.y;
+            }
+          }
         }
+#ifdef XPG_GF_STAMPS
+        if (!(a.dbg & 1))
+#endif
+        if (t + 1 < a.steps) load_block(t + 1, u);
       }
-      if (t + 1 < a.steps) load_block(t + 1, u);
     }
-    // the chunk's waves add their column sums in a fixed tree (wave k += wave k + m)
-    for (int n = nwc; n > 1;) {
-      const int m = (n + 1) >> 1;
-      float* slot = Wt + h * L.slots * 2048;  // this chunk's slots (over its w tables)
-      if (wvalid && k >= m && k < n) {
-        float* s = slot + (k - m) * 2048 + lane;
+    if (aborted) break;
+    GF_STAMP(4)
+    // every wave's column sums to its own slot [b][j] (over the w tables, dead until rebuilt);
+    // the Adam threads add a column's nwc slots in wave order
+    if (wvalid) {
+      float* sl = Wt + (h * nwc + k) * kGfSlot + lane;
 #pragma unroll
-        for (int b = 0; b < 32; ++b) s[b * 64] = acc[b];
-      }
-      lds_barrier();
-      if (wvalid && k < n - m) {
-        const float* s = slot + k * 2048 + lane;
-#pragma unroll
-        for (int b = 0; b < 32; ++b) acc[b] += s[b * 64];
-      }
-      lds_barrier();
-      n = m;
-    }
-    if (wvalid && k == 0) {
-#pragma unroll
-      for (int b = 0; b < 32; ++b) cs[h * 32 * kGfColPitch + b * kGfColPitch + lane] = acc[b];
+      for (int b = 0; b < 32; ++b) sl[b * kGfColPitch] = acc[b];
     }
     lds_barrier();
+    GF_STAMP(5)
     // ---- Adam on the own columns (w before the step counts in the loss's |w| sum)
     double aw = 0.0;
     for (int e = tid; e < CH * 2048; e += kGfThreads) {
       const int hh = e >> 11, el = e & 2047;
       if (hh < nch && c_lo + e < a.cols) {
-        const float gsum = cs[hh * 32 * kGfColPitch + (el & 31) * kGfColPitch + (el >> 5)];
+        const float* sl = Wt + hh * nwc * kGfSlot + (el & 31) * kGfColPitch + (el >> 5);
+        float gsum = sl[0];
+        for (int kk = 1; kk < nwc; ++kk) gsum += sl[kk * kGfSlot];
         float w = Wv[e], m = Mv[e], v = Vv[e];
         aw += fabs(static_cast<double>(w));
         const float sgn = w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f);
@@ -5285,9 +5378,14 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
       for (int i = 0; i < kGfWaves; ++i) s += red[i];
       a.aw_part[(int64_t)t * a.nwg + wg] = s;
     }
+    GF_STAMP(6)
     build_w_tables();
     lds_barrier();
   }
+#ifdef XPG_GF_STAMPS
+  if (tid == 0)
+    for (int i = 0; i < 8; ++i) g_gf_stamps[wg * 8 + i] = gst[i];
+#endif
   if (aborted) return;
   for (int e = tid; e < CH * 2048; e += kGfThreads) {
     const int64_t c = c_lo + e;
@@ -6687,11 +6785,11 @@ static void wlm_plan_fused(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) 
   const int nrbp = static_cast<int>(cdiv(nrb, kGfTpw) * kGfTpw), nwc = nrbp / kGfTpw;
   const int ch_max = std::min(kGfMaxCh, kGfWaves / nwc);
   if (ch_max < 1 || rows > INT32_MAX || cols > INT32_MAX) return;
-  const int64_t cus = device_cus();
+  const int64_t cus = std::min(device_cus(), kGfMaxWg);
   const int64_t ch = cdiv(n_chunks, cus);
   if (ch > ch_max) return;
   const GfLds G = gf_lds(static_cast<int>(ch), nrbp);
-  const size_t lds = sizeof(float) * (size_t)G.total + 2 * kGfWaves * sizeof(double);
+  const size_t lds = sizeof(float) * (size_t)G.total + 2 * kGfWaves * sizeof(double) + sizeof(double);
   if (lds > 160 * 1024) return;
   L->gf = true;
   L->gf_ch = static_cast<int>(ch);
