@@ -5002,6 +5002,10 @@ constexpr int kGfMaxCh = 2;        // chunks per workgroup (LDS: w tables + w / 
 constexpr int kGfWaves = 8;        // waves per workgroup
 constexpr int kGfTpw = 4;          // resident 32-row blocks per wave
 constexpr int kGfThreads = kGfWaves * 64;
+#ifndef XPG_GF_G8
+#define XPG_GF_G8 1
+#endif
+constexpr bool kGfG8 = XPG_GF_G8;  // phase 3 by byte tables (4 lookups per column word)
 constexpr int kGfLook1 = 8;        // phase 1: rows whose 8 lookups issue together
 constexpr int kGfLook3 = 4;        // phase 3: columns whose 8 lookups issue together (acc[32] live)
 constexpr int kGfColPitch = 65;    // column-sum image [b][j] pitch: conflict-free both ways
@@ -5020,7 +5024,8 @@ struct GfArgs {
   int rows, cols, words, steps, batch, ch, nrbp, nwg, fault_wg;
   uint32_t spin_limit;
 #ifdef XPG_GF_STAMPS
-  int dbg;  // diagnostics build: 1 = no next-step bit loads (compute alone)
+  int dbg;  // diagnostics build: 1 = no next-step bit loads (compute alone), 2 = phase-1 / 3
+            // lookups without LDS (the address as the value), 4 = lookups at a fixed address
 #endif
 };
 
@@ -5086,8 +5091,11 @@ __device__ uint64_t g_gf_stamps[1024 * 8];
     glast = now_;                                    \
     __builtin_amdgcn_sched_barrier(0);               \
   }
+#define GF_LOOK(addr, imm, base)                                                             \
+  ((a.dbg & 2) ? __uint_as_float(addr) : (a.dbg & 4) ? lds_f32((base) | (addr & 0u), imm) : lds_f32(addr, imm))
 #else
 #define GF_STAMP(k)
+#define GF_LOOK(addr, imm, base) lds_f32(addr, imm)
 #endif
 
 __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
@@ -5099,6 +5107,8 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform roles and row blocks
   const int wg = blockIdx.x, CH = a.ch, nwc = a.nrbp / kGfTpw;
   const GfLds L = gf_lds(CH, a.nrbp);
+  // phase 3 by byte tables of 8-row groups when they fit over the w tables
+  const bool g8 = kGfG8 && a.nrbp * 4 * 256 <= L.w - L.r0;
   double* red = reinterpret_cast<double*>(gsm + L.total);  // [kGfWaves] aw, [kGfWaves] tk
   // abort flag after the doubles: no static LDS, so the image (and the w tables) start at LDS
   // address 0 and a table address is an and-or of the shifted nibble with the lane's base
@@ -5210,7 +5220,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
                 for (int i = 0; i < kGfLook1; ++i)
 #pragma unroll
                   for (int q = 0; q < 8; ++q)
-                    v[i][q] = lds_f32(and_or(shr_i(x[u][i0 + i1 + i], 4 * q - 8), 0xf00u, tb), q * 4096);
+                    v[i][q] = GF_LOOK(and_or(shr_i(x[u][i0 + i1 + i], 4 * q - 8), 0xf00u, tb), q * 4096, tb);
 #pragma unroll
                 for (int i = 0; i < kGfLook1; i += 2) {  // two rows per packed add
                   f32x2 s2 = {v[i][0], v[i + 1][0]};
@@ -5300,6 +5310,14 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
         G[e] = ((v & 1) ? gg[0] : 0.f) + ((v & 2) ? gg[1] : 0.f) + ((v & 4) ? gg[2] : 0.f) + ((v & 8) ? gg[3] : 0.f);
       }
       lds_barrier();
+      if (g8) {  // byte tables of 8-row groups (over the dead w tables): low + high nibble entries
+        for (int e = tid; e < 256 * (a.nrbp * 4); e += kGfThreads) {
+          const int byte = e & 255, g8i = e >> 8;
+          if (half_of_row(g8i * 8) != H) continue;
+          Wt[e] = G[(2 * g8i) * 16 + (byte & 15)] + G[(2 * g8i + 1) * 16 + (byte >> 4)];
+        }
+        lds_barrier();
+      }
       if (H == 0) GF_STAMP(3)
 #pragma unroll
       for (int u = 2 * H; u < 2 * H + 2; ++u) {
@@ -5310,6 +5328,28 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
           // G[group][v], group = 4 rows: the block's groups at byte gbase + n * 64 (gbase: a
           // multiple of 64, so the nibble's 4-B slot is an and-or)
           const uint32_t gbase = static_cast<uint32_t>(L.G + rb * 8 * 16) * 4u;
+          if (g8) {  // 4 byte lookups per column: G8[group8][byte] at byte g8base + m * 1024
+            const uint32_t g8base = static_cast<uint32_t>(L.r0 + rb * 4 * 256) * 4u;
+#pragma unroll
+            for (int b0 = 0; b0 < 32; b0 += 2 * kGfLook3) {
+              float v[2 * kGfLook3][4];
+#pragma unroll
+              for (int b = 0; b < 2 * kGfLook3; ++b)
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                  v[b][m] = GF_LOOK(and_or(shr_i(x[u][b0 + b], 8 * m - 2), 0x3fcu, g8base), m * 1024, g8base);
+#pragma unroll
+              for (int b = 0; b < 2 * kGfLook3; b += 2) {
+                f32x2 s2 = {v[b][0], v[b + 1][0]};
+#pragma unroll
+                for (int m = 1; m < 4; ++m) s2 += f32x2{v[b][m], v[b + 1][m]};
+                f32x2 a2 = {acc[b0 + b], acc[b0 + b + 1]};
+                a2 += s2;
+                acc[b0 + b] = a2.x;
+                acc[b0 + b + 1] = a2.y;
+              }
+            }
+          } else
 #pragma unroll
           for (int b0 = 0; b0 < 32; b0 += kGfLook3) {
             float v[kGfLook3][8];  // the lookups of kGfLook3 columns in flight, then the adds
@@ -5317,7 +5357,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
             for (int b = 0; b < kGfLook3; ++b)
 #pragma unroll
               for (int n = 0; n < 8; ++n)
-                v[b][n] = lds_f32(and_or(shr_i(x[u][b0 + b], 4 * n - 2), 0x3cu, gbase), n * 64);
+                v[b][n] = GF_LOOK(and_or(shr_i(x[u][b0 + b], 4 * n - 2), 0x3cu, gbase), n * 64, gbase);
 #pragma unroll
             for (int b = 0; b < kGfLook3; b += 2) {  // two columns per packed add
               f32x2 s2 = {v[b][0], v[b + 1][0]};
