@@ -5379,7 +5379,9 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
     if (aborted) break;
     GF_STAMP(4)
     // every wave's column sums to its own slot [b][j] (over the w tables, dead until rebuilt);
-    // the Adam threads add a column's nwc slots in wave order
+    // the Adam threads add a column's nwc slots in wave order.  The byte tables live there too:
+    // every wave's lookups end first
+    if (g8) lds_barrier();
     if (wvalid) {
       float* sl = Wt + (h * nwc + k) * kGfSlot + lane;
 #pragma unroll

@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
   const int nrb = (batch + 31) / 32, nrbp = (nrb + kGfTpw - 1) / kGfTpw * kGfTpw;
   const int ch = (n_chunks + cus - 1) / cus, nwg = (n_chunks + ch - 1) / ch;
   const GfLds L = gf_lds(ch, nrbp);
-  size_t lds = sizeof(float) * L.total + 2 * kGfWaves * sizeof(double);
+  size_t lds = sizeof(float) * L.total + 2 * kGfWaves * sizeof(double) + sizeof(double);
   if (lds < 81 * 1024) lds = 81 * 1024;
   printf("cols %d rows %d batch %d steps %d: ch %d nrbp %d nwg %d lds %zu\n", cols, rows, batch, steps, ch, nrbp, nwg, lds);
   uint32_t* bits; double* kern; WlmStep* stp; float *w, *m, *v, *ph; double *tk, *aw; uint64_t* xp; uint32_t* err;
