@@ -5091,10 +5091,14 @@ __device__ uint64_t g_gf_stamps[1024 * 8];
     glast = now_;                                    \
     __builtin_amdgcn_sched_barrier(0);               \
   }
+#ifdef XPG_GF_ABL  // lookup ablations (dbg 2 / 4): a runtime select per lookup, slower as such
 #define GF_LOOK(addr, imm, base)                                                             \
   ((a.dbg & 2) ? __uint_as_float(addr) : (a.dbg & 4) ? lds_f32((base) | (addr & 0u), imm) : lds_f32(addr, imm))
 #else
-#define GF_STAMP(k)
+#define GF_LOOK(addr, imm, base) lds_f32(addr, imm)
+#endif
+#else
+#define GF_STAMP(k) {}
 #define GF_LOOK(addr, imm, base) lds_f32(addr, imm)
 #endif
 
@@ -5293,7 +5297,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
         if (half_of_row(r) == H)
           gb[r] = r < B ? gf_poll(a.xp + (int64_t)a.batch * a.nwg + r, tag, a.spin_limit, a.err, &abort_s) : 0.f;
       lds_barrier();
-      if (H == 0) GF_STAMP(2)
+      if (H == 0) { GF_STAMP(2) }
       if (abort_s) {
         aborted = true;
         break;
@@ -5318,7 +5322,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
         }
         lds_barrier();
       }
-      if (H == 0) GF_STAMP(3)
+      if (H == 0) { GF_STAMP(3) }
 #pragma unroll
       for (int u = 2 * H; u < 2 * H + 2; ++u) {
         const int rb = kGfTpw * k + u;
