@@ -5003,7 +5003,7 @@ constexpr int kGfWaves = 8;        // waves per workgroup
 constexpr int kGfTpw = 4;          // resident 32-row blocks per wave
 constexpr int kGfThreads = kGfWaves * 64;
 #ifndef XPG_GF_G8
-#define XPG_GF_G8 1
+#define XPG_GF_G8 0
 #endif
 constexpr bool kGfG8 = XPG_GF_G8;  // phase 3 by byte tables (4 lookups per column word)
 constexpr int kGfLook1 = 8;        // phase 1: rows whose 8 lookups issue together
