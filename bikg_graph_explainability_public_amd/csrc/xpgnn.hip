@@ -5002,10 +5002,6 @@ constexpr int kGfMaxCh = 2;        // chunks per workgroup (LDS: w tables + w / 
 constexpr int kGfWaves = 8;        // waves per workgroup
 constexpr int kGfTpw = 4;          // resident 32-row blocks per wave
 constexpr int kGfThreads = kGfWaves * 64;
-#ifndef XPG_GF_G8
-#define XPG_GF_G8 0
-#endif
-constexpr bool kGfG8 = XPG_GF_G8;  // phase 3 by byte tables (4 lookups per column word)
 constexpr int kGfLook1 = 8;        // phase 1: rows whose 8 lookups issue together
 constexpr int kGfLook3 = 4;        // phase 3: columns whose 8 lookups issue together (acc[32] live)
 constexpr int kGfColPitch = 65;    // column-sum image [b][j] pitch: conflict-free both ways
@@ -5111,8 +5107,6 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform roles and row blocks
   const int wg = blockIdx.x, CH = a.ch, nwc = a.nrbp / kGfTpw;
   const GfLds L = gf_lds(CH, a.nrbp);
-  // phase 3 by byte tables of 8-row groups when they fit over the w tables
-  const bool g8 = kGfG8 && a.nrbp * 4 * 256 <= L.w - L.r0;
   double* red = reinterpret_cast<double*>(gsm + L.total);  // [kGfWaves] aw, [kGfWaves] tk
   // abort flag after the doubles: no static LDS, so the image (and the w tables) start at LDS
   // address 0 and a table address is an and-or of the shifted nibble with the lane's base
@@ -5143,22 +5137,24 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
   // the bits of step t's row block kGfTpw * k + u: buffer loads (descriptor at the block's first
   // row in SGPRs, lane word in voffset, row in soffset); rows past the batch re-read its last row
   // (masked at use)
-  auto load_block = [&](int64_t t, int u) {
+  // rows i0 .. i0 + n - 1 of step t's block u (u, i0, n compile-time after unrolling)
+  // No branch: a block past the batch or past the last step (or a wave without a chunk) gets a
+  // descriptor of zero records, whose loads return 0 without touching memory (a conditional
+  // load keeps the registers' old values alive beside the new ones)
+  auto load_rows = [&](int64_t t, int u, int i0, int n) {
     const int64_t r0 = t * a.batch;
-    const int B = static_cast<int>(min((int64_t)a.batch, (int64_t)a.rows - r0));
+    const int B = t < a.steps ? static_cast<int>(min((int64_t)a.batch, (int64_t)a.rows - r0)) : 0;
     const int rb = kGfTpw * k + u;
-    if (wvalid && rb * 32 < B) {
-      const int last = min(32, B - rb * 32) - 1;
-      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint32_t*>(a.bits + (r0 + rb * 32) * (int64_t)a.words), 0,
-          static_cast<int>(pitch * static_cast<uint32_t>(last + 1)), 0x00020000);
+    const int nr = wvalid ? max(0, min(32, B - rb * 32)) : 0, last = max(nr - 1, 0);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(a.bits + (nr > 0 ? (r0 + rb * 32) * (int64_t)a.words : 0)), 0,
+        static_cast<int>(pitch * static_cast<uint32_t>(nr)), 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 32; ++i)
-        x[u][i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wd * 4u, static_cast<uint32_t>(min(i, last)) * pitch, 0);
-    }
+    for (int i = i0; i < i0 + n; ++i)
+      x[u][i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wd * 4u, static_cast<uint32_t>(min(i, last)) * pitch, 0);
   };
 #pragma unroll
-  for (int u = 0; u < kGfTpw; ++u) load_block(0, u);  // in flight during the set-up
+  for (int u = 0; u < kGfTpw; ++u) load_rows(0, u, 0, 32);  // in flight during the set-up
 
   // w / m / v of the own columns into LDS (0 past cols), then the w tables
   for (int e = tid; e < CH * 2048; e += kGfThreads) {
@@ -5314,14 +5310,6 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
         G[e] = ((v & 1) ? gg[0] : 0.f) + ((v & 2) ? gg[1] : 0.f) + ((v & 4) ? gg[2] : 0.f) + ((v & 8) ? gg[3] : 0.f);
       }
       lds_barrier();
-      if (g8) {  // byte tables of 8-row groups (over the dead w tables): low + high nibble entries
-        for (int e = tid; e < 256 * (a.nrbp * 4); e += kGfThreads) {
-          const int byte = e & 255, g8i = e >> 8;
-          if (half_of_row(g8i * 8) != H) continue;
-          Wt[e] = G[(2 * g8i) * 16 + (byte & 15)] + G[(2 * g8i + 1) * 16 + (byte >> 4)];
-        }
-        lds_barrier();
-      }
       if (H == 0) { GF_STAMP(3) }
 #pragma unroll
       for (int u = 2 * H; u < 2 * H + 2; ++u) {
@@ -5332,28 +5320,6 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
           // G[group][v], group = 4 rows: the block's groups at byte gbase + n * 64 (gbase: a
           // multiple of 64, so the nibble's 4-B slot is an and-or)
           const uint32_t gbase = static_cast<uint32_t>(L.G + rb * 8 * 16) * 4u;
-          if (g8) {  // 4 byte lookups per column: G8[group8][byte] at byte g8base + m * 1024
-            const uint32_t g8base = static_cast<uint32_t>(L.r0 + rb * 4 * 256) * 4u;
-#pragma unroll
-            for (int b0 = 0; b0 < 32; b0 += 2 * kGfLook3) {
-              float v[2 * kGfLook3][4];
-#pragma unroll
-              for (int b = 0; b < 2 * kGfLook3; ++b)
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-                  v[b][m] = GF_LOOK(and_or(shr_i(x[u][b0 + b], 8 * m - 2), 0x3fcu, g8base), m * 1024, g8base);
-#pragma unroll
-              for (int b = 0; b < 2 * kGfLook3; b += 2) {
-                f32x2 s2 = {v[b][0], v[b + 1][0]};
-#pragma unroll
-                for (int m = 1; m < 4; ++m) s2 += f32x2{v[b][m], v[b + 1][m]};
-                f32x2 a2 = {acc[b0 + b], acc[b0 + b + 1]};
-                a2 += s2;
-                acc[b0 + b] = a2.x;
-                acc[b0 + b + 1] = a2.y;
-              }
-            }
-          } else
 #pragma unroll
           for (int b0 = 0; b0 < 32; b0 += kGfLook3) {
             float v[kGfLook3][8];  // the lookups of kGfLook3 columns in flight, then the adds
@@ -5372,20 +5338,21 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
               acc[b0 + b] = a2.x;
               acc[b0 + b + 1] = a2.y;
             }
+            // the next step's rows into the registers of the columns consumed so far: half the
+            // block half-way, the rest at the end (a wave stalls issuing its 64th vector memory
+            // op in flight; 32 at a time per block kept it waiting on the fetch)
+            if (b0 == 16 - kGfLook3) load_rows(t + 1, u, 0, 16);
           }
+          load_rows(t + 1, u, 16, 16);
+        } else {
+          load_rows(t + 1, u, 0, 32);
         }
-#ifdef XPG_GF_STAMPS
-        if (!(a.dbg & 1))
-#endif
-        if (t + 1 < a.steps) load_block(t + 1, u);
       }
     }
     if (aborted) break;
     GF_STAMP(4)
     // every wave's column sums to its own slot [b][j] (over the w tables, dead until rebuilt);
-    // the Adam threads add a column's nwc slots in wave order.  The byte tables live there too:
-    // every wave's lookups end first
-    if (g8) lds_barrier();
+    // the Adam threads add a column's nwc slots in wave order
     if (wvalid) {
       float* sl = Wt + (h * nwc + k) * kGfSlot + lane;
 #pragma unroll
