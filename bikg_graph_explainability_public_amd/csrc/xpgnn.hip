@@ -5146,9 +5146,13 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
     const int B = t < a.steps ? static_cast<int>(min((int64_t)a.batch, (int64_t)a.rows - r0)) : 0;
     const int rb = kGfTpw * k + u;
     const int nr = wvalid ? max(0, min(32, B - rb * 32)) : 0, last = max(nr - 1, 0);
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(a.bits + (nr > 0 ? (r0 + rb * 32) * (int64_t)a.words : 0)), 0,
-        static_cast<int>(pitch * static_cast<uint32_t>(nr)), 0x00020000);
+#ifdef XPG_GF_STAMPS
+    const int64_t roff = (a.dbg & 8) ? 0 : (r0 + rb * 32) * (int64_t)a.words;  // dbg 8: always block 0
+#else
+    const int64_t roff = (r0 + rb * 32) * (int64_t)a.words;
+#endif
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.bits + (nr > 0 ? roff : 0)), 0,
+                                                        static_cast<int>(pitch * static_cast<uint32_t>(nr)), 0x00020000);
 #pragma unroll
     for (int i = i0; i < i0 + n; ++i)
       x[u][i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wd * 4u, static_cast<uint32_t>(min(i, last)) * pitch, 0);
