@@ -99,6 +99,17 @@ def launch_ranks(args):
     return subprocess.call(cmd)
 
 
+# XPG_BENCH_RCCL1=1 at one rank: a process group of ONE rank over RCCL, with every N-rank code
+# path (exchange staging, async all-gathers and their stream waits, uneven gathers, max over
+# ranks) taken as at N > 1 -- the RCCL path executed on a one-GPU box (a rehearsal, not a bench)
+RCCL1 = os.environ.get("XPG_BENCH_RCCL1") == "1"
+
+
+def multi(world):
+    """True when the run takes the N-rank code paths (N > 1, or the one-rank RCCL rehearsal)."""
+    return world > 1 or RCCL1
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -106,6 +117,13 @@ def setup_dist(args):
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: launch one rank per "
                          "GPU (python bench.py --gpus N starts them itself)")
+    if world == 1 and RCCL1:
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        return world, rank, 0
     if world > 1:
         import torch.distributed as dist
         # XPG_BENCH_BACKEND=gloo + XPG_BENCH_ONE_GPU=1: a rehearsal of the N-rank path with
@@ -130,7 +148,7 @@ def rank_layout(world, local):
     props = torch.cuda.get_device_properties(local)
     me = {"local_rank": local, "device": local, "name": props.name,
           "pci_bus_id": getattr(props, "pci_bus_id", None), "host": platform.node()}
-    if world == 1:
+    if not multi(world):
         return {"backend": None, "world": 1, "ranks": [me]}
     import torch.distributed as dist
     ranks = [None] * world
@@ -143,14 +161,14 @@ def rank_layout(world, local):
 
 def barrier(world):
     torch.cuda.synchronize()
-    if world > 1:
+    if multi(world):
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
 
 
 def max_over_ranks(x, world, dev):
-    if world == 1:
+    if not multi(world):
         return x
     import torch.distributed as dist
     t = torch.tensor([x], device=dev, dtype=torch.float64)
@@ -404,7 +422,7 @@ def _headline_core(args, dev, world, rank, workload="c2", lanes_ok=True):
     # split form with eager RCCL all-gathers between two graphs (several ranks, or
     # XPG_BENCH_SPLIT_GRAPH=1).
     use_graph = not args.no_graph
-    split = world > 1 or os.environ.get("XPG_BENCH_SPLIT_GRAPH") == "1"
+    split = multi(world) or os.environ.get("XPG_BENCH_SPLIT_GRAPH") == "1"
     # the pipelined graphs need each rank's fits to read only its own rows ((f0, f1) repeats
     # == rows [r0, r1), e.g. times = world): the fit must not regenerate rows from seed_t
     unroll, depth = 1, 1
@@ -525,7 +543,7 @@ def _headline_core(args, dev, world, rank, workload="c2", lanes_ok=True):
             def pick_unroll(n):
                 return next((u for u in range(want, 1, -1) if u % 2 == 0 and n % u == 0), 1)
             n_lanes = 2 if (lanes_ok and os.environ.get("XPG_BENCH_FIT_DEPTH", "2") == "2" and
-                            world == 1 and args.steps % 2 == 0) else 1
+                            not multi(world) and args.steps % 2 == 0) else 1
             depth = n_lanes
             per_lane = args.steps // n_lanes
             unroll = pick_unroll(per_lane)
@@ -547,7 +565,7 @@ def _headline_core(args, dev, world, rank, workload="c2", lanes_ok=True):
                             ws=torch.empty(plan.workspace_bytes(nl), dtype=torch.uint8, device=dev))
             lanes = [make_lane(lane) for lane in range(n_lanes)]
             sets = lanes[0]["sets"]
-            ex = world > 1
+            ex = multi(world)
             if ex:  # staging row: y fp32 [nl] | k fp64 [nl] | w fp32 [nf, S]
                 oy, ok_ = 0, -(-nl * 4 // 8) * 8
                 ow = ok_ + nl * 8
@@ -884,7 +902,7 @@ def c3_section(args, dev, world, rank):
     for _ in range(reps):
         y = plan.forward(bits)
     b.record(stream)
-    logits = y[:, qcols] if world == 1 else _gather_uneven(y[:, qcols].contiguous(), world)
+    logits = y[:, qcols] if not multi(world) else _gather_uneven(y[:, qcols].contiguous(), world)
     torch.cuda.synchronize()
     barrier(world)
     wall = max_over_ranks((time.perf_counter() - t0) / reps, world, dev)
@@ -1776,9 +1794,11 @@ def main():
         order = [n for n in regimes if n != "c3_full_graph"] + \
             (["c3_full_graph"] if "c3_full_graph" in regimes else [])
         line["regimes"] = {n: regimes[n] for n in order}
+    if RCCL1 and world == 1:
+        line["rccl1_rehearsal"] = True
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi(world):
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -67,3 +67,22 @@ def test_bench_two_rank_c3_uneven_shard_matches_one_rank():
     assert c2["rows_per_rank"] == 64  # rank 0's shard (rank 1: 16)
     assert c1["rows_per_rank"] == 80
     assert c2["logits_checksum"] == c1["logits_checksum"]
+
+
+@pytest.mark.gpu
+def test_bench_rccl_one_rank_rehearsal():
+    """The RCCL code path on real hardware: a process group of ONE rank over RCCL
+    (XPG_BENCH_RCCL1=1) takes every N-rank branch of the bench -- the headline's exchange
+    staging and async all-gathers (all_gather_into_tensor on the "nccl" backend, a work handle
+    whose wait() orders the current stream), the c3 uneven all-gather, the max over ranks -- so
+    the collectives the driver's 8-GPU run uses are executed here, and give the 1-rank answers
+    bit for bit (graph / exchange checks 0, c3 logits checksum equal to a plain 1-rank run's)."""
+    rows = ["--c3-rows", "80"]
+    r = _bench(1, "headline,c3", {"XPG_BENCH_RCCL1": "1"}, timeout=170, extra_args=rows)
+    assert r.get("rccl1_rehearsal") is True
+    assert r["rank_layout"]["backend"] == "nccl (RCCL)" and r["rank_layout"]["world"] == 1
+    assert r["graph_check_max_abs_diff"] == 0.0
+    assert r["exchange_check_max_abs_diff"] == 0.0
+    assert r["value"] > 0
+    one = _bench(1, "c3", timeout=120, extra_args=rows)
+    assert r["regimes"]["c3_full_graph"]["logits_checksum"] == one["regimes"]["c3_full_graph"]["logits_checksum"]

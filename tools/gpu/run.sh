@@ -36,6 +36,7 @@ for step in "$@"; do
     wlmtests) run wlmtests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_coverage.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "wlm or run_queries or graph" ;;
     gfprobe) run gfprobe 120 ./tools/gf_probe 1000000 25600 512 3 && run gfprobe_noload 120 ./tools/gf_probe 1000000 25600 512 3 1 && run gfprobe_ns 120 ./tools/gf_probe_ns 1000000 25600 512 3 ;;
     gfabl) for d in 0 1 2 4; do run gfabl_$d 120 ./tools/gf_probe_abl 1000000 25600 512 2 $d || exit 1; done ;;
+    rccl1) run rccl1 400 python -u -m pytest tests/test_gpu_multirank.py -m gpu -v -rf --timeout 360 --timeout-method thread -k rccl_one_rank ;;
     gfl2) run gfl2 120 ./tools/gf_probe 1000000 25600 512 3 8 ;;
     gfg4) run gfg4 120 ./tools/gf_probe_g4 1000000 25600 512 3 && run gfg4_nl 120 ./tools/gf_probe_g4 1000000 25600 512 3 1 ;;
     gfpmc) cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
