@@ -130,6 +130,33 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32]) {
   }
 }
 
+// transpose32 with its 16- and 8-bit stages as byte permutes (v_perm_b32: two per pair instead of
+// the shift / xor / mask sequence); the 4-, 2- and 1-bit stages as in transpose32
+__device__ __forceinline__ void transpose32_perm(uint32_t (&a)[32]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {  // j = 16: halves
+    const uint32_t x = a[k], y = a[k + 16];
+    a[k] = __builtin_amdgcn_perm(y, x, 0x05040100u);
+    a[k + 16] = __builtin_amdgcn_perm(y, x, 0x07060302u);
+  }
+#pragma unroll
+  for (int k = 0; k < 32; k = (k + 9) & ~8) {  // j = 8: bytes
+    const uint32_t x = a[k], y = a[k + 8];
+    a[k] = __builtin_amdgcn_perm(y, x, 0x06020400u);
+    a[k + 8] = __builtin_amdgcn_perm(y, x, 0x07030501u);
+  }
+#pragma unroll
+  for (int j = 4, s = 2; j != 0; j >>= 1, ++s) {
+    const uint32_t m = s == 2 ? 0x0F0F0F0Fu : s == 3 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+    for (int k = 0; k < 32; k = (k + j + 1) & ~j) {
+      const uint32_t t = ((a[k] >> j) ^ a[k + j]) & m;
+      a[k + j] ^= t;
+      a[k] ^= t << j;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------ masks
 __global__ void k_pack(const uint8_t* __restrict__ m, int64_t rows, int64_t cols, int words,
                        uint32_t* __restrict__ bits) {
@@ -5151,11 +5178,19 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
 #else
     const int64_t roff = (r0 + rb * 32) * (int64_t)a.words;
 #endif
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(a.bits + (nr > 0 ? roff : 0)), 0,
-                                                        static_cast<int>(pitch * static_cast<uint32_t>(nr)), 0x00020000);
+    // the descriptor's inputs made provably wave-uniform (readfirstlane): otherwise the compiler
+    // wraps every buffer load in a waterfall loop (cdna_hip_programming.md T20), which cost the
+    // step ~16k cycles of its 128 loads per wave
+    const uint64_t base = reinterpret_cast<uint64_t>(a.bits + (nr > 0 ? roff : 0));
+    const uint32_t blo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base));
+    const uint32_t bhi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane(static_cast<int>(pitch * static_cast<uint32_t>(nr)));
+    const int lastu = __builtin_amdgcn_readfirstlane(last);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<uint32_t*>((static_cast<uint64_t>(bhi) << 32) | blo), 0, bytes, 0x00020000);
 #pragma unroll
     for (int i = i0; i < i0 + n; ++i)
-      x[u][i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wd * 4u, static_cast<uint32_t>(min(i, last)) * pitch, 0);
+      x[u][i] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, wd * 4u, static_cast<uint32_t>(min(i, lastu)) * pitch, 0);
   };
 #pragma unroll
   for (int u = 0; u < kGfTpw; ++u) load_rows(0, u, 0, 32);  // in flight during the set-up
@@ -5320,7 +5355,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
         const int rb = kGfTpw * k + u;
         const int nr = min(32, B - rb * 32);
         if (wvalid && nr > 0) {
-          transpose32(x[u]);  // x[u][b] = column 32 * word + b over the block's rows (masked in phase 1)
+          transpose32_perm(x[u]);  // x[u][b] = column 32 * word + b over the block's rows (masked in phase 1)
           // G[group][v], group = 4 rows: the block's groups at byte gbase + n * 64 (gbase: a
           // multiple of 64, so the nibble's 4-B slot is an and-or)
           const uint32_t gbase = static_cast<uint32_t>(L.G + rb * 8 * 16) * 4u;
