@@ -5015,9 +5015,9 @@ __global__ __launch_bounds__(64) void k_gw_loss(const double* __restrict__ tk_pa
 // owning `ch` chunks of 64 mask words (2048 columns).  Per step:
 //   phase 1  the step's bits of the own chunks are in registers (x[4][32]: a wave holds four
 //            32-row blocks of one chunk, lane = word; 8 waves at up to 256 VGPRs); p partials by
-//            the nibble tables of w (as k_gw_p); each wave publishes its chunk's partials as
-//            tagged 8-B granules {step + 1, p} -> xp[row][chunk]
-//   reduce   row j belongs to workgroup j mod nwg: one wave polls its n_chunks granules, sums them
+//            the nibble tables of w (as k_gw_p), chunk partials added in chunk order, published
+//            as tagged 8-B granules {step + 1, p} -> xp[row][wg]
+//   reduce   row j belongs to workgroup j mod nwg: one wave polls its nwg granules, sums them
 //            (lane-strided, then a fixed butterfly), g_j = k_j cg (p_j - ybar), p_hist, the loss
 //            term; publishes {step + 1, g_j} -> xg[j]
 //   phase 3  every workgroup polls the batch's g, builds 4-row G tables, and the SAME bit
@@ -5039,8 +5039,7 @@ constexpr int kGfLook1 = 8;        // phase 1: rows whose 8 lookups issue togeth
 constexpr int kGfLook3 = 4;        // phase 3: columns whose 8 lookups issue together (acc[32] live)
 constexpr int kGfColPitch = 65;    // column-sum image [b][j] pitch: conflict-free both ways
 constexpr int kGfSlot = 32 * kGfColPitch;  // one wave's column-sum slot (floats)
-constexpr int kGfMaxWg = 512;      // workgroups per fit
-constexpr int kGfMaxChunks = 512;  // chunks per fit (a reducer lane polls n_chunks / 64 granules)
+constexpr int kGfMaxWg = 512;      // workgroups per fit (a reducer lane polls nwg / 64 granules)
 
 struct GfArgs {
   const uint32_t* bits;
@@ -5149,11 +5148,9 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
   const int n_chunks = (a.words + kGwWords - 1) / kGwWords;
   const int chunk0 = wg * CH;
   const int nch = min(CH, n_chunks - chunk0);  // own chunks (>= 1)
-  const int NS = a.nwg * CH;                    // p granule slots per row: one per chunk
   // this wave's role in phases 1 / 3: chunk h, row blocks kGfTpw * k ...
   const int h = wave / nwc, k = wave - h * nwc;
   const bool wvalid = h < nch;
-  uint64_t* const xpw = a.xp + chunk0 + (wvalid ? h : 0);  // this wave's chunk column of p slots
   const int w0 = (chunk0 + (wvalid ? h : 0)) * kGwWords;
   const int nw = min(kGwWords, a.words - w0);
   const uint32_t lmask = lane < nw ? ~0u : 0u;
@@ -5163,6 +5160,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
   float* Wv = gsm + L.w;
   float* Mv = gsm + L.m;
   float* Vv = gsm + L.v;
+  float* pp = gsm + L.pp;
   float* gb = gsm + L.gb;
   float* G = gsm + L.G;
   const int RB = a.nrbp * 32;
@@ -5237,7 +5235,6 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
     const int64_t r0 = (int64_t)t * a.batch;
     const int B = static_cast<int>(min((int64_t)a.batch, (int64_t)a.rows - r0));
     const uint32_t tag = static_cast<uint32_t>(t + 1);
-    const bool pub = !(a.fault_wg == wg && t == 0);  // test hook: a workgroup that never publishes
     GF_STAMP(7)
     double tk = 0.0;
 #pragma unroll
@@ -5280,12 +5277,19 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
               }
               const float tot = wave_transpose_reduce8_pl(c, lane);  // row i0 + (lane >> 3)
               const int i = i0 + (lane >> 3);
-              // the chunk's partial of the row, published by the wave itself (no barrier, no
-              // workgroup sum): granule slot (row, chunk)
-              if (!(lane & 7) && i < nr && pub)
-                st64_sc1(xpw + (rb * 32 + i) * NS, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(tot));
+              if (!(lane & 7) && i < nr) pp[h * RB + rb * 32 + i] = tot;
             }
           }
+        }
+      }
+      lds_barrier();
+      // ---- publish the workgroup's partial of every row of the half (chunks added in order)
+      if (!(a.fault_wg == wg && t == 0)) {
+        for (int r = tid; r < B; r += kGfThreads) {
+          if (half_of_row(r) != H) continue;
+          float v = 0.f;
+          for (int hh = 0; hh < nch; ++hh) v += pp[hh * RB + r];
+          st64_sc1(a.xp + (int64_t)r * a.nwg + wg, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(v));
         }
       }
     }
@@ -5295,15 +5299,15 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
       // ---- reduce the half's rows this workgroup owns: p_j, g_j, the loss term
       for (int j = wg + wave * a.nwg; j < B; j += kGfWaves * a.nwg) {
         if (half_of_row(j) != H) continue;  // wave-uniform
-        const uint64_t* src = a.xp + (int64_t)j * NS;
-        // the lane's chunk granules c = lane + 64 i: all loads in flight first, then any spins
-        uint64_t gr[kGfMaxChunks / 64];
+        const uint64_t* src = a.xp + (int64_t)j * a.nwg;
+        // the lane's granules c = lane + 64 i: all loads in flight first, then any spins
+        uint64_t gr[kGfMaxWg / 64];
 #pragma unroll
-        for (int i = 0; i < kGfMaxChunks / 64; ++i)
-          gr[i] = lane + 64 * i < n_chunks ? ld64_sc1(src + lane + 64 * i) : (static_cast<uint64_t>(tag) << 32);
+        for (int i = 0; i < kGfMaxWg / 64; ++i)
+          gr[i] = lane + 64 * i < a.nwg ? ld64_sc1(src + lane + 64 * i) : (static_cast<uint64_t>(tag) << 32);
         float part = 0.f;
 #pragma unroll
-        for (int i = 0; i < kGfMaxChunks / 64; ++i)
+        for (int i = 0; i < kGfMaxWg / 64; ++i)
           part += static_cast<uint32_t>(gr[i] >> 32) == tag
                       ? __uint_as_float(static_cast<uint32_t>(gr[i]))
                       : gf_poll(src + lane + 64 * i, tag, a.spin_limit, a.err, &abort_s);
@@ -5316,7 +5320,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
           const float g = static_cast<float>(kj * sc.cg * d);
           a.p_hist[r0 + j] = p;
           tk += kj * d * d;
-          st64_sc1(a.xp + (int64_t)a.batch * NS + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(g));
+          st64_sc1(a.xp + (int64_t)a.batch * a.nwg + j, (static_cast<uint64_t>(tag) << 32) | __float_as_uint(g));
         }
       }
     }
@@ -5332,7 +5336,7 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
     for (int H = 0; H < 2; ++H) {
       for (int r = tid; r < RB; r += kGfThreads)
         if (half_of_row(r) == H)
-          gb[r] = r < B ? gf_poll(a.xp + (int64_t)a.batch * NS + r, tag, a.spin_limit, a.err, &abort_s) : 0.f;
+          gb[r] = r < B ? gf_poll(a.xp + (int64_t)a.batch * a.nwg + r, tag, a.spin_limit, a.err, &abort_s) : 0.f;
       lds_barrier();
       if (H == 0) { GF_STAMP(2) }
       if (abort_s) {
@@ -6841,7 +6845,7 @@ static void wlm_plan_fused(int64_t rows, int64_t cols, int64_t batch, WlmWs* L) 
   if (ch_max < 1 || rows > INT32_MAX || cols > INT32_MAX) return;
   const int64_t cus = std::min(device_cus(), kGfMaxWg);
   const int64_t ch = cdiv(n_chunks, cus);
-  if (ch > ch_max || n_chunks > kGfMaxChunks) return;
+  if (ch > ch_max) return;
   const GfLds G = gf_lds(static_cast<int>(ch), nrbp);
   const size_t lds = sizeof(float) * (size_t)G.total + 2 * kGfWaves * sizeof(double) + sizeof(double);
   if (lds > 160 * 1024) return;
@@ -6880,7 +6884,7 @@ static int wlm_layout_grid(int64_t n_fits, int64_t rows, int64_t cols, int64_t b
   L->aw_off = off;
   off += align_up(F * sizeof(double) * (size_t)steps * n_part);
   L->gfx_off = off;  // fused: per fit [batch][nwg] p granules + [batch] g granules
-  off += align_up(L->gf ? F * sizeof(uint64_t) * (size_t)batch * ((size_t)L->gf_nwg * L->gf_ch + 1) : 0);
+  off += align_up(L->gf ? F * sizeof(uint64_t) * (size_t)batch * (L->gf_nwg + 1) : 0);
   L->gferr_off = off;
   off += align_up(L->gf ? sizeof(uint32_t) : 0);
   L->total = off;
@@ -7002,7 +7006,7 @@ static int wlm_fit_grid(int64_t n_fits, const uint32_t* bits, int64_t rows, int6
   if (L.gf) {
     uint64_t* gx = reinterpret_cast<uint64_t*>(ws + L.gfx_off);
     uint32_t* err = reinterpret_cast<uint32_t*>(ws + L.gferr_off);
-    const int64_t n_gx = (int64_t)batch * ((int64_t)L.gf_nwg * L.gf_ch + 1);  // [batch][chunk slots] + g
+    const int64_t n_gx = (int64_t)batch * (L.gf_nwg + 1);
     // per-step constants + granule / error-word clearing, one launch
     hipLaunchKernelGGL(k_wlm_stats, dim3(static_cast<unsigned>(steps), nf), dim3(256), 0, st, y, kernel, rows, ib,
                        P, step0, stp, gx, n_gx * n_fits, err, 1);

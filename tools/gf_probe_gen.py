@@ -59,7 +59,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&w, 4 * (size_t)cols)); CK(hipMalloc(&m, 4 * (size_t)cols)); CK(hipMalloc(&v, 4 * (size_t)cols));
   CK(hipMalloc(&ph, 4 * (size_t)rows));
   CK(hipMalloc(&tk, 8 * (size_t)steps * nwg)); CK(hipMalloc(&aw, 8 * (size_t)steps * nwg));
-  CK(hipMalloc(&xp, 8 * (size_t)batch * (nwg + 1))); CK(hipMalloc(&err, 4));
+  const size_t n_xp = (size_t)batch * ((size_t)nwg + 1);  // [batch][workgroup slots] + g granules
+  CK(hipMalloc(&xp, 8 * n_xp)); CK(hipMalloc(&err, 4));
   hipLaunchKernelGGL(fill_bits, dim3(4096), dim3(256), 0, 0, bits, (size_t)rows * words, 7u);
   std::vector<double> hk(rows, 1e-3);
   CK(hipMemcpy(kern, hk.data(), 8 * rows, hipMemcpyHostToDevice));
@@ -87,7 +88,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int r = 0; r < reps; ++r) {
     CK(hipMemset(w, 0, 4 * (size_t)cols)); CK(hipMemset(m, 0, 4 * (size_t)cols)); CK(hipMemset(v, 0, 4 * (size_t)cols));
-    CK(hipMemset(xp, 0, 8 * (size_t)batch * (nwg + 1))); CK(hipMemset(err, 0, 4));
+    CK(hipMemset(xp, 0, 8 * n_xp)); CK(hipMemset(err, 0, 4));
     CK(hipEventRecord(e0));
     hipLaunchKernelGGL(k_gw_fused, dim3(nwg), dim3(kGfThreads), lds, 0, a);
     CK(hipEventRecord(e1));
