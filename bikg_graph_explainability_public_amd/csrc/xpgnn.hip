@@ -6290,7 +6290,16 @@ int launch_shapley(uint64_t seed, int64_t row_offset, int64_t rows, int64_t cols
     XPG_LAUNCHED();
     return XPG_OK;
   }
-  const dim3 grid(static_cast<unsigned>(cdiv(quads, 256)), static_cast<unsigned>(std::min<int64_t>(rows, 65535)));
+  // rows per block: each thread makes 16 B per row, so one row per block (25,600 x 31 blocks at
+  // the c3 graph_prediction shape) left the kernel at the block-dispatch rate; the blocks now
+  // stride over rows, ~64 per CU (XPG_SHAPLEY_BLOCKS, a diagnostics switch: total blocks, -1 =
+  // one row per block; bits are the same either way: counter-based per (quad, row))
+  const int64_t gx = cdiv(quads, 256);
+  int env_blk = 0;
+  if (const int rc = diag_env("XPG_SHAPLEY_BLOCKS", &env_blk)) return rc;
+  const int64_t nblk = env_blk != 0 ? env_blk : 64 * (int64_t)device_cus();
+  const int64_t gy = nblk > 0 ? std::max<int64_t>(1, std::min<int64_t>(rows, nblk / gx)) : std::min<int64_t>(rows, 65535);
+  const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(std::min<int64_t>(gy, 65535)));
   if (words % 4 == 0)
     hipLaunchKernelGGL(k_shapley<4>, grid, dim3(256), 0, st, seed, row_offset, rows, cols, words, bits, counts, seed_dev);
   else if (words % 2 == 0)
