@@ -43,6 +43,7 @@ for step in "$@"; do
            run gfpmc1 120 timeout -s KILL 60 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU --kernel-trace --output-format csv -d gpurun_out/gfpmc1 -o run -- ./tools/gf_probe_ns 1000000 25600 512 2 && \
            run gfpmc2 120 timeout -s KILL 60 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/gfpmc2 -o run -- ./tools/gf_probe_ns 1000000 25600 512 2 ;;
     samptests) run samptests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_coverage.py -m gpu -q -rf --timeout 300 --timeout-method thread -k "shapley or sampler or mask or seed" ;;
+    shaptests) run shaptests 400 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -k "shap or kernel or golden or explainer_run" ;;
     gftests) run gftests 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v -rf --timeout 300 --timeout-method thread -k "fused or (oracle_large and grid) or (continuation and grid) or many_columns" ;;
     gpsec) for r in 1 2; do run gp_$r 300 python bench.py --sections gp --no-cpu-baseline; done ;;
     early2) run early2 500 python -u tools/ws_ab.py --rows 64 --reps 3 --variants "OVERLAP=0;OVERLAP=0,EARLY2=1;OVERLAP=0;OVERLAP=0,EARLY2=1;OVERLAP=1;OVERLAP=1,EARLY2=1" ;;
