@@ -622,24 +622,36 @@ __device__ __forceinline__ double shap_approx_row(int64_t k, int64_t Mi, int ref
 // int(0.9 * 1000), ... at which the sum is != 0, i.e. (as above) at which any row's value is
 // != 0, so that ref is the minimum over rows of each row's first such level.  Pass A (grid, thread
 // per row): the row's first level at which its value is != 0 (levels past the last ref > 0: a
-// sentinel), written over out[r]; pass B (one block): the minimum level, then every row's value at
+// sentinel; 16 lanes per row, each walking every 16th level), written over out[r]; pass B (one
+// block): the minimum level, then every row's value at
 // that ref (at the last ref > 0 when no row ever is != 0: the values the sequential loop leaves,
 // all == 0).  At S = 1M columns every row underflows to 0 for tens of levels: a one-block loop
 // recomputing all rows at each level took 130 us for 25,600 rows (round 5); here each row walks
 // its own levels.
 constexpr double kShapNoLevel = 1e9;
-__global__ void k_shap_approx_levels(const int32_t* __restrict__ cnt, int64_t rows, int64_t cols,
-                                     double* __restrict__ out) {
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (r >= rows) return;
-  const int64_t Mi = cols - 1, k = cnt[r];
+constexpr int kShapLanes = 16;  // lanes per row in pass A: lane s walks levels s, s + 16, ...
+// grid of rows x 16 lanes (256-thread blocks); a row's lanes are 16 consecutive lanes of a wave
+__global__ __launch_bounds__(256) void k_shap_approx_levels(const int32_t* __restrict__ cnt, int64_t rows,
+                                                            int64_t cols, double* __restrict__ out) {
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t r = gid / kShapLanes;
+  const int sub = static_cast<int>(gid % kShapLanes);
   double lev = kShapNoLevel;
-  for (int ref = 1000, l = 0; ref > 0; ref = static_cast<int>(0.9 * static_cast<double>(ref)), ++l)
-    if (!(shap_approx_row(k, Mi, ref) == 0.0)) {
-      lev = static_cast<double>(l);
-      break;
+  if (r < rows) {
+    const int64_t Mi = cols - 1, k = cnt[r];
+    int ref = 1000;
+    for (int i = 0; i < sub && ref > 0; ++i) ref = static_cast<int>(0.9 * static_cast<double>(ref));
+    for (int l = sub; ref > 0; l += kShapLanes) {
+      if (!(shap_approx_row(k, Mi, ref) == 0.0)) {  // this lane's first: its levels ascend
+        lev = static_cast<double>(l);
+        break;
+      }
+      for (int i = 0; i < kShapLanes && ref > 0; ++i) ref = static_cast<int>(0.9 * static_cast<double>(ref));
     }
-  out[r] = lev;
+  }
+#pragma unroll
+  for (int o = kShapLanes / 2; o > 0; o >>= 1) lev = fmin(lev, __shfl_xor(lev, o));  // the row's first
+  if (r < rows && sub == 0) out[r] = lev;
 }
 
 __global__ __launch_bounds__(1024) void k_shap_approx_pick(const int32_t* __restrict__ cnt, int64_t rows,
@@ -6597,8 +6609,8 @@ int xpg_shap_kernel(const int32_t* counts, int64_t rows, int64_t cols, double* k
     hipLaunchKernelGGL(k_shap_exact, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream), counts,
                        rows, cols, kernel_out);
   else {
-    hipLaunchKernelGGL(k_shap_approx_levels, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0,
-                       S(stream), counts, rows, cols, kernel_out);
+    hipLaunchKernelGGL(k_shap_approx_levels, dim3(static_cast<unsigned>(cdiv(rows * kShapLanes, 256))), dim3(256),
+                       0, S(stream), counts, rows, cols, kernel_out);
     XPG_LAUNCHED();
     hipLaunchKernelGGL(k_shap_approx_pick, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
     XPG_LAUNCHED();
