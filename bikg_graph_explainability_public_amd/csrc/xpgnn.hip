@@ -613,68 +613,38 @@ __device__ __forceinline__ double shap_approx_row(int64_t k, int64_t Mi, int ref
   return M / (choose * static_cast<double>(k) * static_cast<double>(Mi - k));
 }
 
-// The reference's loop `while sum(kernel) == 0 and ref > 0` (kernels.py:148-162): row values are
-// >= 0, +inf, or negative for an all-active row (k = M + 1, quirk Q5), and a sum holding a NaN
-// or an infinity is != 0, so the sum is != 0 exactly when some row's value is != 0 (the sum of
-// non-zero values cancelling to exactly 0 is the only case this reads differently, and the
-// reference's own float summation order would decide that case).
-// The back-off loop in parallel: the reference stops at the first ref of the sequence 1000,
-// int(0.9 * 1000), ... at which the sum is != 0, i.e. (as above) at which any row's value is
-// != 0, so that ref is the minimum over rows of each row's first such level.  Pass A (grid, thread
-// per row): the row's first level at which its value is != 0 (levels past the last ref > 0: a
-// sentinel; 16 lanes per row, each walking every 16th level), written over out[r]; pass B (one
-// block): the minimum level, then every row's value at
-// that ref (at the last ref > 0 when no row ever is != 0: the values the sequential loop leaves,
-// all == 0).  At S = 1M columns every row underflows to 0 for tens of levels: a one-block loop
-// recomputing all rows at each level took 130 us for 25,600 rows (round 5); here each row walks
-// its own levels.
-constexpr double kShapNoLevel = 1e9;
-constexpr int kShapLanes = 16;  // lanes per row in pass A: lane s walks levels s, s + 16, ...
-// grid of rows x 16 lanes (256-thread blocks); a row's lanes are 16 consecutive lanes of a wave
-__global__ __launch_bounds__(256) void k_shap_approx_levels(const int32_t* __restrict__ cnt, int64_t rows,
-                                                            int64_t cols, double* __restrict__ out) {
-  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t r = gid / kShapLanes;
-  const int sub = static_cast<int>(gid % kShapLanes);
-  double lev = kShapNoLevel;
-  if (r < rows) {
-    const int64_t Mi = cols - 1, k = cnt[r];
-    int ref = 1000;
-    for (int i = 0; i < sub && ref > 0; ++i) ref = static_cast<int>(0.9 * static_cast<double>(ref));
-    for (int l = sub; ref > 0; l += kShapLanes) {
-      if (!(shap_approx_row(k, Mi, ref) == 0.0)) {  // this lane's first: its levels ascend
-        lev = static_cast<double>(l);
-        break;
-      }
-      for (int i = 0; i < kShapLanes && ref > 0; ++i) ref = static_cast<int>(0.9 * static_cast<double>(ref));
-    }
-  }
-#pragma unroll
-  for (int o = kShapLanes / 2; o > 0; o >>= 1) lev = fmin(lev, __shfl_xor(lev, o));  // the row's first
-  if (r < rows && sub == 0) out[r] = lev;
+// pass 1 (grid): every row at ref = 1000 (raw values, +-inf kept for the sum test)
+__global__ void k_shap_approx_rows(const int32_t* __restrict__ cnt, int64_t rows, int64_t cols,
+                                   double* __restrict__ out) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r < rows) out[r] = shap_approx_row(cnt[r], cols - 1, 1000);
 }
 
-__global__ __launch_bounds__(1024) void k_shap_approx_pick(const int32_t* __restrict__ cnt, int64_t rows,
-                                                           int64_t cols, double* __restrict__ out) {
-  __shared__ double red[16];
-  double m = kShapNoLevel;
-  for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) m = fmin(m, out[r]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  m = kShapNoLevel;
-  for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) m = fmin(m, red[i]);
-  // the ref of level m, or the last ref > 0 of the sequence
-  int ref = 1000;
-  for (int l = 0;; ++l) {
-    const int nxt = static_cast<int>(0.9 * static_cast<double>(ref));
-    if (static_cast<double>(l) >= m || !(nxt > 0)) break;
-    ref = nxt;
-  }
+// pass 2 (one block): the reference's loop `while sum(kernel) == 0 and ref > 0` (kernels.py:
+// 148-162).  Row values are >= 0, +inf, or negative for an all-active row (k = M + 1, quirk Q5),
+// and a sum holding a NaN or an infinity is != 0: the block scans 1024-row chunks until one
+// holds a value that is not == 0 (normally the first), instead of summing every row (the sum
+// of non-zero values cancelling to exactly 0 is the only case this reads differently, and the
+// reference's own float summation order would decide that case); the ref = int(0.9 ref)
+// back-off recomputes rows in-block.
+__global__ __launch_bounds__(1024) void k_shap_approx_finish(const int32_t* __restrict__ cnt,
+                                                             int64_t rows, int64_t cols,
+                                                             double* __restrict__ out) {
   const int64_t Mi = cols - 1;
-  __syncthreads();  // every thread read out[] before it is overwritten
-  for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) out[r] = shap_approx_row(cnt[r], Mi, ref);
+  int ref = 1000;
+  for (;;) {
+    bool found = false;
+    for (int64_t base = 0; base < rows && !found; base += blockDim.x) {  // block-uniform
+      const int64_t r = base + threadIdx.x;
+      found = __syncthreads_or(r < rows && !(out[r] == 0.0)) != 0;
+    }
+    if (found) break;
+    ref = static_cast<int>(0.9 * static_cast<double>(ref));
+    if (!(ref > 0)) break;  // the sum is 0 here
+    __syncthreads();
+    for (int64_t r = threadIdx.x; r < rows; r += blockDim.x) out[r] = shap_approx_row(cnt[r], Mi, ref);
+    __syncthreads();
+  }
 }
 
 // pass 3 (grid): +-inf / NaN -> 0 (kernels.py:172)
@@ -6609,10 +6579,10 @@ int xpg_shap_kernel(const int32_t* counts, int64_t rows, int64_t cols, double* k
     hipLaunchKernelGGL(k_shap_exact, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream), counts,
                        rows, cols, kernel_out);
   else {
-    hipLaunchKernelGGL(k_shap_approx_levels, dim3(static_cast<unsigned>(cdiv(rows * kShapLanes, 256))), dim3(256),
-                       0, S(stream), counts, rows, cols, kernel_out);
+    hipLaunchKernelGGL(k_shap_approx_rows, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream),
+                       counts, rows, cols, kernel_out);
     XPG_LAUNCHED();
-    hipLaunchKernelGGL(k_shap_approx_pick, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
+    hipLaunchKernelGGL(k_shap_approx_finish, dim3(1), dim3(1024), 0, S(stream), counts, rows, cols, kernel_out);
     XPG_LAUNCHED();
     hipLaunchKernelGGL(k_shap_clean, dim3(static_cast<unsigned>(cdiv(rows, 256))), dim3(256), 0, S(stream), rows,
                        kernel_out);
