@@ -1256,6 +1256,7 @@ def graph_prediction_section(args, dev):
     w0 = torch.zeros(N, device=dev)
     params = {"lr": 0.01, "l1_lambda": 1e-4}
     stream = torch.cuda.current_stream()
+    status = torch.zeros(1, dtype=torch.int32, device=dev)  # sticky fit status, read after timing
 
     def rep(i, ev=None):
         mk = (lambda j: ev[j].record(stream)) if ev else (lambda j: None)
@@ -1266,7 +1267,7 @@ def graph_prediction_section(args, dev):
         mk(2)
         k = engine.shap_kernel(bits, N, counts=cnt)
         mk(3)
-        engine.wlm_fit(bits, N, batch, y, k, w0, params, check=False)
+        engine.wlm_fit(bits, N, batch, y, k, w0, params, check=False, status=status)
         mk(4)
 
     rep(0)
@@ -1278,6 +1279,7 @@ def graph_prediction_section(args, dev):
     torch.cuda.synchronize()
     ph = {name: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in evs]))
           for j, name in enumerate(("sample", "forward", "shap", "wlm"))}
+    engine.check_fit_status(status)  # a fit whose exchange timed out raises (after the timing)
     total = sum(ph.values())
     W = (N + 31) // 32
     kind, parts = engine.wlm_plan(1, R, N, batch)
@@ -1291,6 +1293,7 @@ def graph_prediction_section(args, dev):
                         "interpret_samples=512 x epochs=50 = 25,600 rows, one repeat",
             "ms_per_repeat": total, "samples_per_s": R / (total * 1e-3), "phases_ms": ph,
             "surrogate_fit": "%s (%d workgroup(s) per fit)" % (kind, parts),
+            "fit_status": "clean (sticky status word of every fit checked after the timed repeats)",
             "roofline": dict(roofline(wbytes, ph["wlm"] * 1e-3, "gp", kernels),
                              kernel="many-column surrogate fit (" + ", ".join(kernels) + ")",
                              bytes_formula=formula),
