@@ -5209,16 +5209,28 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
     Mv[e] = ok ? a.mg[c] : 0.f;
     Vv[e] = ok ? a.vg[c] : 0.f;
   }
+  // thread = (chunk hh, nibble q, word j); 512 threads = one chunk per pass, unrolled so both
+  // chunks' w reads are in flight together
+  static_assert(kGfThreads == 8 * 64, "one chunk's tables per pass");
   auto build_w_tables = [&]() {
-    for (int task = tid; task < CH * 8 * 64; task += kGfThreads) {
-      const int hh = task >> 9, q = (task >> 6) & 7, j = task & 63;
-      const float* wq = Wv + hh * 2048 + 32 * j + 4 * q;
-      const float a0 = wq[0], a1 = wq[1], a2 = wq[2], a3 = wq[3];
-      float* Tq = Wt + ((hh * 8 + q) * 16) * 64 + j;
+    const int q = tid >> 6, j = tid & 63;
+    float aq[kGfMaxCh][4];
 #pragma unroll
-      for (int v = 0; v < 16; ++v)
-        Tq[v * 64] = ((v & 1) ? a0 : 0.f) + ((v & 2) ? a1 : 0.f) + ((v & 4) ? a2 : 0.f) + ((v & 8) ? a3 : 0.f);
-    }
+    for (int hh = 0; hh < kGfMaxCh; ++hh)
+      if (hh < CH) {
+        const float* wq = Wv + hh * 2048 + 32 * j + 4 * q;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) aq[hh][b] = wq[b];
+      }
+#pragma unroll
+    for (int hh = 0; hh < kGfMaxCh; ++hh)
+      if (hh < CH) {
+        const float a0 = aq[hh][0], a1 = aq[hh][1], a2 = aq[hh][2], a3 = aq[hh][3];
+        float* Tq = Wt + ((hh * 8 + q) * 16) * 64 + j;
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          Tq[v * 64] = ((v & 1) ? a0 : 0.f) + ((v & 2) ? a1 : 0.f) + ((v & 4) ? a2 : 0.f) + ((v & 8) ? a3 : 0.f);
+      }
   };
   lds_barrier();
   build_w_tables();
@@ -5405,26 +5417,75 @@ __global__ __launch_bounds__(kGfThreads) void k_gw_fused(GfArgs a) {
     }
     lds_barrier();
     GF_STAMP(5)
-    // ---- Adam on the own columns (w before the step counts in the loss's |w| sum)
+    // ---- Adam on the own columns (w before the step counts in the loss's |w| sum).  A runtime
+    // loop over the thread's columns (with the next step's bits live, 128 VGPRs, a fully unrolled
+    // form had no registers to keep its reads in flight and spilled); the nwc slot reads and
+    // w / m / v are issued together for the common slot counts (a runtime slot loop waited for
+    // each read), then added in wave order
+    // two columns (e, e + 512: the same chunk) per iteration, their reads issued together and
+    // their Adam chains interleaved (one column's sqrt / division sequence is serial); computed
+    // branch-free, stored (and counted in the |w| sum) for columns below cols
+    auto slot_sum2 = [&](const float* sl0, const float* sl1, float& g0, float& g1, auto nwc_c) {
+      constexpr int NW = decltype(nwc_c)::value;
+      float s0[NW], s1[NW];
+#pragma unroll
+      for (int kk = 0; kk < NW; ++kk) {
+        s0[kk] = sl0[kk * kGfSlot];
+        s1[kk] = sl1[kk * kGfSlot];
+      }
+      g0 = s0[0];
+      g1 = s1[0];
+#pragma unroll
+      for (int kk = 1; kk < NW; ++kk) {
+        g0 += s0[kk];
+        g1 += s1[kk];
+      }
+    };
+    static_assert((2048 / kGfThreads) % 2 == 0, "column pairs within a chunk");
     double aw = 0.0;
-    for (int e = tid; e < CH * 2048; e += kGfThreads) {
-      const int hh = e >> 11, el = e & 2047;
-      if (hh < nch && c_lo + e < a.cols) {
-        const float* sl = Wt + hh * nwc * kGfSlot + (el & 31) * kGfColPitch + (el >> 5);
-        float gsum = sl[0];
-        for (int kk = 1; kk < nwc; ++kk) gsum += sl[kk * kGfSlot];
-        float w = Wv[e], m = Mv[e], v = Vv[e];
-        aw += fabs(static_cast<double>(w));
-        const float sgn = w > 0.f ? 1.f : (w < 0.f ? -1.f : 0.f);
-        float gr = fmaf(l1s, sgn, gsum);
-        gr = fmaf(a.P.weight_decay, w, gr);
-        m = fmaf(1.f - a.P.beta1, gr - m, m);
-        v = fmaf(1.f - a.P.beta2, gr * gr, v * a.P.beta2);
-        const float denom = sqrtf(v) / sc.bc2_sqrt + a.P.eps;
-        w = w - sc.step_size * (m / denom);
-        Wv[e] = w;
-        Mv[e] = m;
-        Vv[e] = v;
+    for (int e0 = tid; e0 < CH * 2048; e0 += 2 * kGfThreads) {
+      const int hh = e0 >> 11;
+      if (hh >= nch) break;  // wave-uniform; chunks ascend with e0
+      float w[2], m[2], v[2], gs[2];
+      const float* sl[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int e = e0 + j * kGfThreads, el = e & 2047;
+        sl[j] = Wt + hh * nwc * kGfSlot + (el & 31) * kGfColPitch + (el >> 5);
+        w[j] = Wv[e];
+        m[j] = Mv[e];
+        v[j] = Vv[e];
+      }
+      if (nwc == 4) slot_sum2(sl[0], sl[1], gs[0], gs[1], std::integral_constant<int, 4>{});
+      else if (nwc == 2) slot_sum2(sl[0], sl[1], gs[0], gs[1], std::integral_constant<int, 2>{});
+      else if (nwc == 8) slot_sum2(sl[0], sl[1], gs[0], gs[1], std::integral_constant<int, 8>{});
+      else {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          gs[j] = sl[j][0];
+          for (int kk = 1; kk < nwc; ++kk) gs[j] += sl[j][kk * kGfSlot];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = c_lo + e0 + j * kGfThreads < a.cols;
+        aw += ok ? fabs(static_cast<double>(w[j])) : 0.0;
+        const float sgn = w[j] > 0.f ? 1.f : (w[j] < 0.f ? -1.f : 0.f);
+        float gr = fmaf(l1s, sgn, gs[j]);
+        gr = fmaf(a.P.weight_decay, w[j], gr);
+        m[j] = fmaf(1.f - a.P.beta1, gr - m[j], m[j]);
+        v[j] = fmaf(1.f - a.P.beta2, gr * gr, v[j] * a.P.beta2);
+        const float denom = sqrtf(v[j]) / sc.bc2_sqrt + a.P.eps;
+        w[j] = w[j] - sc.step_size * (m[j] / denom);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int e = e0 + j * kGfThreads;
+        if (c_lo + e < a.cols) {
+          Wv[e] = w[j];
+          Mv[e] = m[j];
+          Vv[e] = v[j];
+        }
       }
     }
 #pragma unroll
