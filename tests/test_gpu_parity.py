@@ -720,11 +720,14 @@ def test_wlm_fit_many_columns_vs_oracle():
 
 @pytest.mark.parametrize("F,R,S,B", [(1, 2500, 20_000, 1000),   # 32 row blocks: one chunk per workgroup
                                      (1, 1100, 70_000, 96),     # 3 row blocks, short last batch
-                                     (3, 1024, 17_000, 512)])   # 3 fits: one launch each
+                                     (3, 1024, 17_000, 512),    # 3 fits: one launch each
+                                     (1, 1500, 20_000, 320),    # 3 waves per chunk (runtime slot sum)
+                                     (1, 1400, 40_000, 700)])   # 6 waves per chunk, one chunk
 def test_wlm_fit_fused_grid_shapes_vs_oracle(F, R, S, B):
     """The persistent many-column fit (k_gw_fused) on shapes at its limits vs the fp64 oracle:
     the largest batch it holds in registers, a batch that is not a multiple of 32 with a short
-    last batch, several fits in one call."""
+    last batch, several fits in one call, and waves per chunk (column-sum slots added by Adam)
+    outside the unrolled counts 2 / 4 / 8."""
     e = _eng()
     kind, parts = e.wlm_plan(F, R, S, B)
     assert kind == "grid_fused" and parts >= 1, (kind, parts)
