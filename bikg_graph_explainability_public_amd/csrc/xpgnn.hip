@@ -2843,9 +2843,12 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
         while (m) {  // group-uniform
           float rr[RI][NFI];
           float cv[RI];
+          // a round's empty slots re-read its first kept row: a row layer 1 wrote (h1 holds rows
+          // only for the samples that keep the node; 0 x an unwritten row may be 0 x NaN)
+          const int jf = __builtin_ctz(m);
 #pragma unroll
           for (int q = 0; q < RI; ++q) {
-            const int j = m ? __builtin_ctz(m) : 0;
+            const int j = m ? __builtin_ctz(m) : jf;
             cv[q] = m ? 1.f : 0.f;
             m &= m - 1u;
             const float* sp = base0 + (int64_t)XPG_WDIAG_ROW(ix[j]) * RS + fo;
@@ -2875,9 +2878,10 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
           while (mm) {
             float rr[RI][NFI];
             float cv[RI];
+            const int jf = __builtin_ctz(mm);  // empty slots: the round's first kept row (above)
 #pragma unroll
             for (int q = 0; q < RI; ++q) {
-              const int j = mm ? __builtin_ctz(mm) : 0;
+              const int j = mm ? __builtin_ctz(mm) : jf;
               cv[q] = mm ? 1.f : 0.f;
               mm &= mm - 1u;
               const int srow = __shfl(esrc, lb + j, 64);
@@ -3030,9 +3034,12 @@ __global__ __launch_bounds__(64 * (GW + 4), (GW + 4) / 4) void k_wide_last_ws(co
       while (m) {  // group-uniform
         float rr[RI][NFI];
         float cv[RI];
+        // empty slots re-read the round's first kept row: a written row (h1 holds rows only for
+        // the samples that keep the node; 0 x an unwritten row may be 0 x NaN)
+        const int jf = __builtin_ctz(m);
 #pragma unroll
         for (int q = 0; q < RI; ++q) {
-          const int j = m ? __builtin_ctz(m) : 0;
+          const int j = m ? __builtin_ctz(m) : jf;
           cv[q] = m ? 1.f : 0.f;
           m &= m - 1u;
           const int srow = __shfl(esrc, lb + j, 64);

@@ -810,6 +810,36 @@ def _wide_plan(N=20_000, E=200_000, F=128, seed=4):
     return pipeline.build_plan(arch.to(DEV), x.to(DEV), ei.to(DEV), list(range(N)))
 
 
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_wide_forward_independent_of_workspace_contents(overlap):
+    """The wide path writes h1 rows only for the samples that keep a node (plus one inactive row
+    per node), so its reads must never touch an unwritten row, not even multiplied by 0 (a
+    NaN there made 0 x row NaN: a workspace reused from other data gave wrong outputs).  The
+    same forward into workspaces pre-filled with zeros, NaN bytes and random bytes: bitwise
+    equal, pass overlap on and off."""
+    e = _eng()
+    plan = _wide_plan()
+    bits = e.sample_shapley(41, 96, plan.cols, DEV)
+    nb = plan.workspace_bytes(96)
+    outs = []
+    with _env(XPG_WIDE_OVERLAP=overlap):
+        for fill in ("zero", "nan", "rand"):
+            ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+            if fill == "zero":
+                ws.zero_()
+            elif fill == "nan":
+                ws.fill_(0xFF)
+            else:
+                ws.random_(0, 256, generator=torch.Generator(device=DEV).manual_seed(5))
+            out = torch.empty((96, plan.n_out), dtype=torch.float32, device=DEV)
+            plan.forward(bits, out=out, workspace=ws)
+            outs.append(out)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(outs[0]).all())
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+
+
 def test_wide_forward_two_threads_two_streams():
     """The wide path's pass overlap shares one side stream and its hand-off events per device:
     two host threads forwarding (96 rows = three 32-row passes, so both buffer sets and the
