@@ -147,6 +147,54 @@ def test_hub_targets_all_nodes(kind, dims, fc, path, monkeypatch):
                                    err_msg=f"node {n} (in-degree {indeg[n]})")
 
 
+def _ws_fill(ws, fill):
+    if fill == "zero":
+        ws.zero_()
+    elif fill == "nan":
+        ws.fill_(0xFF)
+    else:
+        ws.random_(0, 256, generator=torch.Generator(device=DEV).manual_seed(5))
+
+
+@pytest.mark.parametrize("path", ["wide", "wide-gather", "wide-exact", "unfused", "rows", "fused"])
+def test_forward_paths_independent_of_workspace_contents(path, monkeypatch):
+    """Every forward path into caller workspaces pre-filled with zeros, NaN bytes and random
+    bytes gives bitwise the same outputs: no kernel reads workspace bytes it did not write
+    (not even multiplied by 0).  All-targets plans on the hub graph (in-degrees past the wide
+    layer 2's list and staging: its in-place rounds) with 70 rows = two 32-row passes + a
+    partial one; single-query plans for the rows / fused paths."""
+    from bikg_graph_explainability_public_amd import pipeline
+    from bikg_graph_explainability_public_amd.nn import ConvStack
+    _force(monkeypatch, path)
+    e = _eng()
+    if path in ("rows", "fused"):
+        S, dims, fc = 500, [8, 16], [16, 1]
+        ei = power_law_graph(S, 1500, {0: 300, 1: 140}, seed=7)
+        targets = [0]
+    else:
+        S, dims, fc = 2500, [24, 128, 128], [128, 1]
+        ei = power_law_graph(S, 15000, {0: 700, 1: 300, 2: 257, 3: 140}, seed=152)
+        targets = list(range(S))
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((S, dims[0]), generator=g)
+    torch.manual_seed(11)
+    arch = ConvStack("sage" if path not in ("rows", "fused") else "gcn", dims, fc).eval()
+    plan = pipeline.build_plan(arch.to(DEV), x.to(DEV), torch.as_tensor(ei).to(DEV), targets)
+    bits = e.pack_masks(torch.as_tensor(_masks(70, S, 3)).to(DEV))
+    nb = plan.workspace_bytes(70)
+    outs = []
+    for fill in ("zero", "nan", "rand"):
+        ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=DEV)
+        _ws_fill(ws, fill)
+        out = torch.empty((70, plan.n_out), dtype=torch.float32, device=DEV)
+        plan.forward(bits, out=out, workspace=ws)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(outs[0]).all())
+    for f, o in zip(("nan", "rand"), outs[1:]):
+        assert torch.equal(o, outs[0]), f
+
+
 @pytest.mark.parametrize("path", ["rows", "fused", "unfused"])
 @pytest.mark.parametrize("kind,dims,fc", [("gcn", [8, 16], [16, 1]),
                                            ("sage", [8, 16, 16], [16, 4, 1]),
@@ -825,12 +873,7 @@ def test_wide_forward_independent_of_workspace_contents(overlap):
     with _env(XPG_WIDE_OVERLAP=overlap):
         for fill in ("zero", "nan", "rand"):
             ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
-            if fill == "zero":
-                ws.zero_()
-            elif fill == "nan":
-                ws.fill_(0xFF)
-            else:
-                ws.random_(0, 256, generator=torch.Generator(device=DEV).manual_seed(5))
+            _ws_fill(ws, fill)
             out = torch.empty((96, plan.n_out), dtype=torch.float32, device=DEV)
             plan.forward(bits, out=out, workspace=ws)
             outs.append(out)
