@@ -1000,3 +1000,54 @@ def test_explainer_clear_cache_sees_param_data_edits():
     df2, _ = fresh.run("7", 1)
     np.testing.assert_allclose(df["config_value_mean"].to_numpy(),
                                df2.loc[df.index, "config_value_mean"].to_numpy(), rtol=0, atol=1e-6)
+
+
+def _poison_scratch(fill):
+    """Fill the engine's shared per-device scratch (the fits' and the k-hop extraction's
+    workspace, reused across entry points) with a byte pattern; grown first so the calls below
+    reuse it."""
+    ws = _eng()._workspace(DEV, 256 << 20)
+    _ws_fill(ws, fill)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("wlm_path,R,S,B", [("mc", 12800, 1193, 256), ("single", 640, 200, 64),
+                                            ("grid", 1500, 20_000, 320), ("grid3", 1024, 17_000, 512)])
+def test_wlm_fit_independent_of_scratch_contents(wlm_path, R, S, B, monkeypatch):
+    """The surrogate fits run in the engine's shared scratch, which holds whatever the previous
+    user left: with it pre-filled with zeros, NaN bytes and random bytes the weights, losses and
+    best epoch are bitwise the same (every exchange slot, counter and staged vector the fit
+    reads is written or cleared by the fit itself)."""
+    monkeypatch.setenv("XPG_WLM", wlm_path)
+    e = _eng()
+    rng = np.random.default_rng(17)
+    m = rng.random((R, S)) < 0.5
+    y = torch.as_tensor(rng.random(R).astype(np.float32))
+    k = torch.as_tensor(oracle.shap_kernel(m))
+    w0 = torch.as_tensor(((rng.random(S) - 0.5) * 0.05).astype(np.float32))
+    params = {"lr": 0.01, "l1_lambda": 1e-4}
+    bits = e.pack_masks(torch.as_tensor(m).to(DEV))
+    res = []
+    for fill in ("zero", "nan", "rand"):
+        _poison_scratch(fill)
+        w, losses, best, _, _ = e.wlm_fit(bits, S, B, y, k, w0, params)
+        res.append((w.clone(), losses.clone(), int(best)))
+    for f, (w, losses, best) in zip(("nan", "rand"), res[1:]):
+        assert torch.equal(w, res[0][0]), f
+        assert torch.equal(losses, res[0][1]), f
+        assert best == res[0][2], f
+
+
+def test_khop_independent_of_scratch_contents():
+    """The k-hop extraction in the shared scratch: the same subgraph whatever the scratch held."""
+    e = _eng()
+    g = torch.Generator().manual_seed(9)
+    N, E = 50_000, 400_000
+    ei = torch.randint(0, N, (2, E), generator=g).to(DEV)
+    res = []
+    for fill in ("zero", "nan", "rand"):
+        _poison_scratch(fill)
+        res.append([t.clone() for t in e.khop_subgraph(7, 3, ei, N)])
+    for f, r in zip(("nan", "rand"), res[1:]):
+        for a, b in zip(r, res[0]):
+            assert torch.equal(a, b), f
