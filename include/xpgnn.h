@@ -263,7 +263,8 @@ int xpg_forward_workspace(const xpg_forward_plan* plan, int64_t rows, size_t* by
 /* y[r * n_last + i] = model output (column out_col) of target i of the last conv layer for
  * mask row r (n_last = layers[n_layers-1].n_tgt; 1 for a single query); with edge_dot set,
  * y[r] = the decoded score of the target pair (dot_a, dot_b).  The workspace also holds the
- * launch's block-scheduling counters (zeroed on the stream before the kernel): calls that may
+ * launch's block-scheduling counters (zeroed on the stream before the kernel); its prior
+ * contents never matter (no kernel reads a workspace byte it did not write).  Calls that may
  * run at the same time (different streams) need workspaces of their own.  Concurrent calls from
  * several host threads are safe under that rule: the wide path's shared side stream and pass
  * events are held by one call's whole enqueue sequence at a time. */
